@@ -1,0 +1,103 @@
+/* sputnik-amd C-ABI: the FFI boundary of the block-sparse matmul hot path.
+ *
+ * Every entry point is extern "C", takes plain structs/pointers/ints and a
+ * hipStream_t (passed as void*), and returns a hipError_t value as int
+ * (0 == hipSuccess). No torch or C++ types cross this boundary. These are the
+ * symbols a ctypes / cgo / JNI binding of the reference's sputnik::block API
+ * would bind; INTEGRATION.md shows the bindings.
+ *
+ * Struct layouts are byte-identical to the C++ descriptors in
+ * include/sputnik/block/arguments.h (reference sputnik/block/arguments.h:48-162):
+ *   sputnik_block_matrix_t: 88 bytes, fields at 0,4,8,12,16,24,...,72,80
+ *   sputnik_matrix_t:       16 bytes, fields at 0,4,8
+ *
+ * Error behaviour: where the reference aborts (missing transposed-metadata or
+ * row-index workspace: dsd_..._tn_align8.cu:73-75, sdd_..._nn_align8.cu:75;
+ * no compatible kernel: dsd/cutlass/dsd.cu:68-73) these functions return
+ * hipErrorInvalidValue (1) instead; unsupported shapes/block sizes return
+ * hipErrorNotSupported (801) exactly as the reference does (dsd.cu:16,
+ * block_gemm.h:728-745).
+ */
+#ifndef SPUTNIK_AMD_H_
+#define SPUTNIK_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sputnik_block_matrix {
+  int32_t rows;        /* elements */
+  int32_t cols;        /* elements */
+  int32_t nonzeros;    /* elements = #blocks * block_size^2 */
+  int32_t block_size;  /* 16/32/64/128; only 128 is accepted by the ops */
+  void *data;          /* #blocks * bs * bs values, block-major, row-major blocks */
+  void *offsets;       /* int32[rows/bs + 1] (in blocks) */
+  void *indices;       /* int16[#blocks] block-column */
+  void *offsets_t;     /* int32[cols/bs + 1] */
+  void *indices_t;     /* int16[#blocks] */
+  void *block_offsets; /* int32[#blocks] */
+  void *row_indices;   /* int16[#blocks] */
+  void *bitmask;       /* unused by this library */
+  uint8_t create_metadata; /* C++ bool */
+} sputnik_block_matrix_t;
+
+typedef struct sputnik_matrix {
+  int32_t rows;
+  int32_t cols;
+  void *data;
+} sputnik_matrix_t;
+
+enum {
+  SPUTNIK_DTYPE_F16 = 0,
+  SPUTNIK_DTYPE_BF16 = 1,
+};
+
+/* ---- DSD: C = op(A_bcsr) * op(B)   (reference sputnik/block/dsd/dsd.h:10-22) */
+int sputnik_dsd(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream);
+/* MatmulEx: uses a's precomputed transposed metadata (create_metadata=false). */
+int sputnik_dsd_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream);
+
+/* ---- DDS: C = op(A) * op(B_bcsr)   (reference sputnik/block/dds/dds.h:10-22) */
+int sputnik_dds(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream);
+int sputnik_dds_ex(const sputnik_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream);
+
+/* ---- SDD: C_bcsr = op(A) * op(B) at C's nonzero blocks
+ *      (reference sputnik/block/sdd/sdd.h:10-15; needs c->row_indices) */
+int sputnik_sdd(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream);
+
+/* ---- Metadata builders */
+/* reference sputnik/block/row_indices/row_indices.h:10 */
+int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
+                        void *stream);
+/* reference sputnik/block/transpose/transpose.h:10 (device, bit-identical) */
+int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream);
+
+/* ---- Host-only queries (no GPU work; safe without a device) */
+/* 1 when the reference would accept the problem (same rules as
+ * can_launch_* + ValidMatmul), 0 otherwise. op: 0=DSD 1=DDS 2=SDD. */
+int sputnik_can_implement(int op, const void *a, int transpose_a,
+                          const void *b, int transpose_b, const void *c);
+/* sizeof / offsetof of the descriptors, for ABI checks by bindings. */
+size_t sputnik_abi_block_matrix_size(void);
+size_t sputnik_abi_block_matrix_offset(int field);
+size_t sputnik_abi_matrix_size(void);
+const char *sputnik_version(void);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* SPUTNIK_AMD_H_ */

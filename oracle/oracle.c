@@ -1,0 +1,191 @@
+/* sputnik-amd ORACLE — test infrastructure only, never the product path.
+ *
+ * A plain-C restatement of the reference's host-side algorithms for the
+ * block-sparse hot path. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg load this library (as the checker / the timed CPU
+ * baseline). The product (sputnik_amd/libsputnik.so) never links it.
+ *
+ * Parity status: PARTIALLY PINNED. The reference cannot be built here (its
+ * GPU path needs nvcc + CUTLASS, its host utilities need the CUDA runtime and
+ * absl headers; see DESIGN.md "Oracle") and ships no golden vectors
+ * (SURVEY.md §8(c)). The transpose-metadata restatement is pinned by the one
+ * known-answer vector recorded from the reference's own Transpose in SURVEY.md
+ * §8(c); everything else is a line-by-line restatement of the cited code,
+ * cross-checked by properties (tests/test_oracle.py).
+ *
+ * Every function cites the reference lines it restates.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Mask -> BCSR. sputnik/matrix_utils.cu:254-289 (MakeSparseMatrixRandomUniform
+ * after the shuffle), with row_padding = 1 (block/matrix_utils.cu:41-45 and
+ * every test/benchmark use pad_rows_to=1, so no padding is inserted).
+ * Element (i, j) of the block grid is nonzero iff perm[i*cols + j] < nnz.
+ * Writes offsets[rows+1] and indices[nnz]; returns the number of nonzeros. */
+int oracle_mask_to_bcsr(int rows, int cols, int nnz, const int64_t *perm,
+                        int32_t *offsets, int32_t *indices) {
+  int64_t offset = 0;
+  offsets[0] = 0;
+  for (int64_t i = 0; i < rows; ++i) {
+    for (int64_t j = 0; j < cols; ++j) {
+      if (perm[i * cols + j] < nnz) {
+        indices[offset] = (int32_t)j;
+        ++offset;
+      }
+    }
+    offsets[i + 1] = (int32_t)offset;
+  }
+  return (int)offset;
+}
+
+/* Per-block row index. sputnik/block/row_indices/row_indices.cu:16-18
+ * (and the identical host helper transpose.cu:21-33). */
+void oracle_row_indices(int block_rows, const int32_t *offsets,
+                        int16_t *row_indices) {
+  for (int i = 0; i < block_rows; ++i)
+    for (int off = offsets[i]; off < offsets[i + 1]; ++off)
+      row_indices[off] = (int16_t)i;
+}
+
+/* Transposed-iteration metadata. sputnik/block/transpose/transpose.cu:87-104:
+ *   gather = stable_argsort(indices)            (:89, Argsort :11-19)
+ *   indices_t = row_indices[gather]             (:90-93)
+ *   block_offsets = iota[gather] = gather       (:99-100)
+ *   offsets_t = cumsum(histogram(indices))      (:103-104, :51-66)
+ * The stable argsort is a counting sort by column that visits blocks in
+ * storage order, which is exactly std::stable_sort's order for equal keys. */
+void oracle_transpose(int block_rows, int block_cols, const int32_t *offsets,
+                      const int16_t *indices, int32_t *offsets_t,
+                      int16_t *indices_t, int32_t *block_offsets) {
+  const int blocks = offsets[block_rows];
+  int32_t *cursor = (int32_t *)calloc((size_t)block_cols + 1, sizeof(int32_t));
+  for (int k = 0; k < blocks; ++k) ++cursor[indices[k] + 1];
+  offsets_t[0] = 0;
+  for (int c = 0; c < block_cols; ++c) {
+    offsets_t[c + 1] = offsets_t[c] + cursor[c + 1];
+    cursor[c] = offsets_t[c];
+  }
+  for (int r = 0; r < block_rows; ++r) {
+    for (int k = offsets[r]; k < offsets[r + 1]; ++k) {
+      const int pos = cursor[indices[k]]++;
+      indices_t[pos] = (int16_t)r;
+      block_offsets[pos] = k;
+    }
+  }
+  free(cursor);
+}
+
+/* BCSR -> dense row-major. sputnik/block/matrix_utils.h:81-112 (ToMatrix):
+ * block l of block-row i lands at rows i*bd.., cols indices[l]*bd.., values
+ * read row-major from values + l*bd*bd. */
+void oracle_bcsr_to_dense(int rows, int cols, int bd, const int32_t *offsets,
+                          const int16_t *indices, const float *values,
+                          float *out) {
+  memset(out, 0, sizeof(float) * (size_t)rows * cols);
+  const int brows = rows / bd;
+  for (int i = 0; i < brows; ++i) {
+    for (int l = offsets[i]; l < offsets[i + 1]; ++l) {
+      const float *blk = values + (size_t)l * bd * bd;
+      const int j = indices[l] * bd;
+      for (int br = 0; br < bd; ++br)
+        for (int bc = 0; bc < bd; ++bc)
+          out[(size_t)(i * bd + br) * cols + j + bc] = blk[br * bd + bc];
+    }
+  }
+}
+
+/* Reference matmul. sputnik/matrix_utils.h:376-391 (Matrix::operator*):
+ *   double acc = 0; for l: acc += (float)(a(i,l) * b(l,j)); out = (float)acc
+ * with op(X) = X.T() (matrix_utils.cu:635-643) when the flag is set; reading
+ * the untransposed storage with swapped indices gives the same operands.
+ * The product is a float product (both operands float) promoted to double.
+ *
+ * Zero-skipping: when a_mask / b_mask are given (one byte per 128x128 block
+ * of op(A) [m/128][k/128] / op(B) [k/128][n/128]), k-blocks whose product
+ * block is all-zero are skipped. A skipped term is float(+-0) added to a
+ * double, which leaves a nonzero accumulator unchanged, so the result is the
+ * dense reference's result (up to the sign of an exact zero).
+ * out_mask ([m/128][n/128], optional) restricts the work to those output
+ * blocks (SDD; other entries are left untouched).
+ * threads > 1 uses OpenMP over output rows (CPU-baseline timing only). */
+void oracle_gemm(int m, int n, int k, const float *a, int ta, const float *b,
+                 int tb, const uint8_t *a_mask, const uint8_t *b_mask,
+                 const uint8_t *out_mask, float *out, int threads) {
+  const int kb = (k + 127) / 128;
+  const int nb = (n + 127) / 128;
+  const int64_t lda = ta ? m : k;
+  const int64_t ldb = tb ? k : n;
+#ifdef _OPENMP
+  if (threads < 1) threads = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+#endif
+  for (int i = 0; i < m; ++i) {
+    const int ib = i / 128;
+    for (int j = 0; j < n; ++j) {
+      const int jb = j / 128;
+      if (out_mask && !out_mask[(int64_t)ib * nb + jb]) continue;
+      double acc = 0.0;
+      for (int lb = 0; lb < kb; ++lb) {
+        if (a_mask && !a_mask[(int64_t)ib * kb + lb]) continue;
+        if (b_mask && !b_mask[(int64_t)lb * nb + jb]) continue;
+        const int l1 = (lb + 1) * 128 < k ? (lb + 1) * 128 : k;
+        for (int l = lb * 128; l < l1; ++l) {
+          const float av = ta ? a[(int64_t)l * lda + i] : a[(int64_t)i * lda + l];
+          const float bv = tb ? b[(int64_t)j * ldb + l] : b[(int64_t)l * ldb + j];
+          const float prod = av * bv;
+          acc += (double)prod;
+        }
+      }
+      out[(int64_t)i * n + j] = (float)acc;
+    }
+  }
+}
+
+/* __float2half_rn / __float2bfloat16_rn on the host (round to nearest even),
+ * used to build the fp16/bf16 operands the GPU sees
+ * (sputnik/matrix_utils.cu:40-44 ConvertKernel). Returns the rounded value as
+ * a float. */
+static float round_f16(float x) {
+  union { float f; uint32_t u; } v = {x};
+  const uint32_t sign = v.u & 0x80000000u;
+  v.u &= 0x7fffffffu;
+  if (v.u >= 0x7f800000u) { v.u |= sign; return v.f; } /* inf / nan */
+  if (v.f >= 65520.0f) { v.u = 0x7f800000u | sign; return v.f; }
+  /* Quantum: 2^(e-10) for normal halves, 2^-24 for subnormals. */
+  int e = (int)((v.u >> 23) & 0xff) - 127;
+  if (e < -14) e = -14;
+  const float q = ldexpf(1.0f, e - 10);
+  const float r = nearbyintf(v.f / q) * q; /* exact scaling, RNE */
+  union { float f; uint32_t u; } o = {r};
+  o.u |= sign;
+  return o.f;
+}
+
+static float round_bf16(float x) {
+  union { float f; uint32_t u; } v = {x};
+  if ((v.u & 0x7fffffffu) > 0x7f800000u) return x; /* nan */
+  const uint32_t lsb = (v.u >> 16) & 1u;
+  v.u = (v.u + 0x7fffu + lsb) & 0xffff0000u;
+  return v.f;
+}
+
+void oracle_round(const float *in, float *out, int64_t n, int dtype) {
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = dtype == 1 ? round_bf16(in[i]) : round_f16(in[i]);
+}
+
+int oracle_openmp_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

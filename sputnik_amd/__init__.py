@@ -1,0 +1,306 @@
+"""sputnik_amd — MI355X-native block-sparse matmul (DSD / DDS / SDD, block 128).
+
+Python mirror of the reference's ``sputnik::block`` API (sputnik/sputnik.h,
+sputnik/block/arguments.h) over the C-ABI of ``libsputnik.so``
+(include/sputnik_amd.h). Names, argument meaning and the overload set follow
+the reference:
+
+    Matmul(BlockMatrix a, ta, Matrix b, tb, Matrix c)        DSD  dsd.h:10-15
+    Matmul(Matrix a, ta, BlockMatrix b, tb, Matrix c)        DDS  dds.h:10-15
+    Matmul(Matrix a, ta, Matrix b, tb, BlockMatrix c)        SDD  sdd.h:10-15
+    MatmulEx(...)      (DSD/DDS, precomputed transposed metadata)
+    RowIndices(a, row_indices), Transpose(a)
+    AllocateTransposeBuffers(a), AllocateRowIndicesBuffer(a)
+
+Device memory is held in torch tensors (plumbing only); every computation runs
+in the HIP kernels of libsputnik.so. There is no CPU fallback: if the library
+is missing, importing the compute entry points raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsputnik.so")
+
+hipSuccess = 0
+hipErrorInvalidValue = 1
+hipErrorNotSupported = 801
+
+
+class SputnikError(RuntimeError):
+    """A non-zero hipError_t returned by libsputnik."""
+
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with hipError_t {code}")
+        self.code = code
+
+
+class BlockSize(enum.IntEnum):
+    """reference sputnik/block/arguments.h:13-19"""
+
+    kNone = 0
+    k16 = 16
+    k32 = 32
+    k64 = 64
+    k128 = 128
+
+
+def AsInt(b) -> int:  # noqa: N802 (reference name)
+    b = int(b)
+    return b if b in (16, 32, 64, 128) else 0
+
+
+class _CBlockMatrix(ctypes.Structure):
+    """sputnik_block_matrix_t — byte-identical to the C++ BlockMatrix (88 B)."""
+
+    _fields_ = [
+        ("rows", ctypes.c_int32),
+        ("cols", ctypes.c_int32),
+        ("nonzeros", ctypes.c_int32),
+        ("block_size", ctypes.c_int32),
+        ("data", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("indices", ctypes.c_void_p),
+        ("offsets_t", ctypes.c_void_p),
+        ("indices_t", ctypes.c_void_p),
+        ("block_offsets", ctypes.c_void_p),
+        ("row_indices", ctypes.c_void_p),
+        ("bitmask", ctypes.c_void_p),
+        ("create_metadata", ctypes.c_uint8),
+    ]
+
+
+class _CMatrix(ctypes.Structure):
+    """sputnik_matrix_t (16 B)."""
+
+    _fields_ = [
+        ("rows", ctypes.c_int32),
+        ("cols", ctypes.c_int32),
+        ("data", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_SIGNATURES = {
+    "sputnik_dsd": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dsd_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dds": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dds_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_sdd": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_row_indices": [_P, _P, _P],
+    "sputnik_transpose": [_P, _P],
+    "sputnik_can_implement": [ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_abi_block_matrix_size": [],
+    "sputnik_abi_block_matrix_offset": [ctypes.c_int],
+    "sputnik_abi_matrix_size": [],
+    "sputnik_version": [],
+}
+_RESTYPES = {
+    "sputnik_abi_block_matrix_size": ctypes.c_size_t,
+    "sputnik_abi_block_matrix_offset": ctypes.c_size_t,
+    "sputnik_abi_matrix_size": ctypes.c_size_t,
+    "sputnik_version": ctypes.c_char_p,
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsputnik.so (built by `make -C sputnik_amd`). Raises if absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C sputnik_amd`. There is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = handle
+    return _lib
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+@dataclass
+class Matrix:
+    """Dense row-major matrix (reference arguments.h:155-162)."""
+
+    rows: int
+    cols: int
+    data: object  # torch.Tensor (fp16/bf16), rows*cols elements
+
+    def _c(self) -> _CMatrix:
+        return _CMatrix(self.rows, self.cols, _ptr(self.data))
+
+
+@dataclass
+class BlockMatrix:
+    """BCSR matrix (reference arguments.h:48-153). rows/cols/nonzeros in
+    elements; offsets int32 [rows/b+1]; indices int16 [#blocks]; data holds
+    #blocks row-major b x b blocks back to back."""
+
+    rows: int
+    cols: int
+    block_size: int
+    nonzeros: int
+    data: object
+    offsets: object
+    indices: object
+    offsets_t: object = None
+    indices_t: object = None
+    block_offsets: object = None
+    row_indices: object = None
+    bitmask: object = None
+    create_metadata: bool = True
+
+    @property
+    def num_blocks(self) -> int:
+        b = AsInt(self.block_size)
+        return self.nonzeros // (b * b) if b else 0
+
+    def _c(self) -> _CBlockMatrix:
+        return _CBlockMatrix(
+            self.rows, self.cols, self.nonzeros, int(self.block_size),
+            _ptr(self.data), _ptr(self.offsets), _ptr(self.indices),
+            _ptr(self.offsets_t), _ptr(self.indices_t),
+            _ptr(self.block_offsets), _ptr(self.row_indices),
+            _ptr(self.bitmask), 1 if self.create_metadata else 0)
+
+
+def _dtype_code(t) -> int:
+    import torch
+
+    if t.dtype == torch.float16:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise TypeError(f"unsupported element type {t.dtype} (fp16 or bf16)")
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is not None:
+        return int(stream)
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(code: int, what: str) -> None:
+    if code != hipSuccess:
+        raise SputnikError(code, what)
+
+
+def _call(ex: bool, a, transpose_a: bool, b, transpose_b: bool, c, stream):
+    L = lib()
+    ta, tb = int(bool(transpose_a)), int(bool(transpose_b))
+    if isinstance(a, BlockMatrix) and isinstance(b, Matrix) and isinstance(c, Matrix):
+        ca, cb, cc = a._c(), b._c(), c._c()
+        fn = L.sputnik_dsd_ex if ex else L.sputnik_dsd
+        code = fn(ctypes.byref(ca), ta, ctypes.byref(cb), tb, ctypes.byref(cc),
+                  _dtype_code(b.data), _stream(stream))
+        _check(code, "dsd")
+        return
+    if isinstance(a, Matrix) and isinstance(b, BlockMatrix) and isinstance(c, Matrix):
+        ca, cb, cc = a._c(), b._c(), c._c()
+        fn = L.sputnik_dds_ex if ex else L.sputnik_dds
+        code = fn(ctypes.byref(ca), ta, ctypes.byref(cb), tb, ctypes.byref(cc),
+                  _dtype_code(a.data), _stream(stream))
+        _check(code, "dds")
+        return
+    if (not ex and isinstance(a, Matrix) and isinstance(b, Matrix)
+            and isinstance(c, BlockMatrix)):
+        ca, cb, cc = a._c(), b._c(), c._c()
+        code = L.sputnik_sdd(ctypes.byref(ca), ta, ctypes.byref(cb), tb,
+                             ctypes.byref(cc), _dtype_code(a.data),
+                             _stream(stream))
+        _check(code, "sdd")
+        return
+    raise TypeError("no Matmul overload for these operand kinds")
+
+
+def Matmul(a, transpose_a, b, transpose_b, c, stream=None):  # noqa: N802
+    """DSD / DDS / SDD by operand kinds, like the C++ overload set."""
+    _call(False, a, transpose_a, b, transpose_b, c, stream)
+
+
+def MatmulEx(a, transpose_a, b, transpose_b, c, stream=None):  # noqa: N802
+    """DSD / DDS with the transposed metadata already present."""
+    _call(True, a, transpose_a, b, transpose_b, c, stream)
+
+
+def RowIndices(a: BlockMatrix, row_indices, stream=None):  # noqa: N802
+    """reference sputnik/block/row_indices/row_indices.h:10"""
+    ca = a._c()
+    _check(lib().sputnik_row_indices(ctypes.byref(ca), _ptr(row_indices),
+                                     _stream(stream)), "RowIndices")
+
+
+def Transpose(a: BlockMatrix, stream=None):  # noqa: N802
+    """reference sputnik/block/transpose/transpose.h:10 (on the device)."""
+    ca = a._c()
+    _check(lib().sputnik_transpose(ctypes.byref(ca), _stream(stream)),
+           "Transpose")
+
+
+def AllocateTransposeBuffers(a: BlockMatrix):  # noqa: N802
+    """reference arguments.h:233-245 (torch-owned device workspaces)."""
+    import torch
+
+    dev = a.offsets.device
+    bcols = a.cols // AsInt(a.block_size)
+    a.offsets_t = torch.empty(bcols + 1, dtype=torch.int32, device=dev)
+    a.indices_t = torch.empty(a.num_blocks, dtype=torch.int16, device=dev)
+    a.block_offsets = torch.empty(a.num_blocks, dtype=torch.int32, device=dev)
+
+
+def FreeTransposeBuffers(a: BlockMatrix):  # noqa: N802
+    a.offsets_t = a.indices_t = a.block_offsets = None
+
+
+def AllocateRowIndicesBuffer(a: BlockMatrix):  # noqa: N802
+    """reference arguments.h:259-263"""
+    import torch
+
+    a.row_indices = torch.empty(a.num_blocks, dtype=torch.int16,
+                                device=a.offsets.device)
+
+
+def FreeRowIndicesBuffer(a: BlockMatrix):  # noqa: N802
+    a.row_indices = None
+
+
+_OPS = {"dsd": 0, "dds": 1, "sdd": 2}
+
+
+def can_implement(op: str, a, transpose_a, b, transpose_b, c) -> bool:
+    """Host-only: would the library accept this problem? (no device work)"""
+    ca, cb, cc = a._c(), b._c(), c._c()
+    return bool(lib().sputnik_can_implement(
+        _OPS[op], ctypes.byref(ca), int(bool(transpose_a)), ctypes.byref(cb),
+        int(bool(transpose_b)), ctypes.byref(cc)))
+
+
+def version() -> str:
+    return lib().sputnik_version().decode()
+
+
+__all__ = [
+    "AllocateRowIndicesBuffer", "AllocateTransposeBuffers", "AsInt",
+    "BlockMatrix", "BlockSize", "FreeRowIndicesBuffer",
+    "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",
+    "SputnikError", "Transpose", "can_implement", "lib", "version",
+]

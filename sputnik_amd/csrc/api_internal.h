@@ -1,0 +1,42 @@
+// sputnik-amd: host entry points shared by the C++ API and the C-ABI.
+#ifndef SPUTNIK_AMD_API_INTERNAL_H_
+#define SPUTNIK_AMD_API_INTERNAL_H_
+
+#include "sputnik/block/arguments.h"
+
+namespace sputnik_amd {
+
+// Outcome of the host-side acceptance checks of one call.
+enum class Status {
+  kOk,
+  kNotSupported,     // block size != 128 -> hipErrorNotSupported (dsd.cu:16)
+  kNoKernel,         // reference: "No compatible kernel" -> abort
+  kMissingMetadata,  // reference: SPUTNIK_CHECK(offsets_t ...) -> abort
+  kMissingRowIndices,
+};
+
+using sputnik::block::BlockMatrix;
+using sputnik::block::Matrix;
+
+// Validate, optionally build transposed metadata, launch. A non-kOk *status
+// means nothing was launched.
+hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const Matrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *status);
+hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const Matrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *status);
+hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, hipStream_t stream,
+                  Status *status);
+
+// hipError_t value the C-ABI returns for a status (never aborts).
+int StatusCode(Status st);
+
+// Host-only acceptance test. op 0 = DSD, 1 = DDS, 2 = SDD.
+bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
+                  const void *c);
+
+}  // namespace sputnik_amd
+
+#endif  // SPUTNIK_AMD_API_INTERNAL_H_

@@ -1,0 +1,467 @@
+// sputnik-amd: the block-sparse GEMM kernel for gfx950 (CDNA4, MI355X).
+//
+// One kernel template serves every product of the hot path. It computes an
+// output tile O[i][j] = sum_k S[i][k] * D[k][j] of 128 x BN, where
+//   S = the "row operand": one 128-row block-row of a BCSR matrix (DSD, DDS)
+//       or a 128-row panel of a dense matrix (SDD),
+//   D = the dense operand, a BN-wide panel,
+// and writes O either straight (DSD), transposed (DDS computes C^T = B^T A^T)
+// or into one 128x128 block of a BCSR output (SDD).
+//
+// It replaces the whole CUTLASS stack of the reference:
+//   BlockGemm::operator()              block_gemm.h:749-878
+//   ConfigHelper / OutputConfig        block_gemm.h:22-510
+//   BlockTileAccessIterator            block_tile_access_iterator.h:23-322
+//   DependentTileAccessIterator        dependent_tile_access_iterator.h:12-178
+//   BlockTileOutputIterator (+epilogue) block_tile_output_iterator.h:18-230
+//   swizzles                            threadblock_swizzle.h:6-69
+// but is designed for CDNA4, not translated:
+//   * 64-wide waves; 2 x (BN/64) waves, each owning a 64x64 sub-tile computed
+//     with v_mfma_f32_16x16x32_{f16,bf16} (4x4 accumulators of 16x16).
+//   * Operands stream HBM/L2 -> LDS with buffer_load_dwordx4 ... lds (LDS-DMA,
+//     no VGPR staging) into a 3-stage ring of BK=64 slices, kept in flight
+//     across raw s_barriers with counted vmcnt waits.
+//   * Partial tiles (N, M, K not multiples of the tile) are zero-filled by the
+//     buffer unit's range check (out-of-range lanes read 0), so the MFMA loop
+//     never branches on bounds.
+//   * Each operand is read from LDS in whichever orientation it has in HBM:
+//     k-contiguous images with ds_read_b128, m/n-contiguous images with the
+//     gfx950 transpose read ds_read_b64_tr_b16. Both images are XOR-swizzled
+//     on the DMA source address so every read is bank-conflict free.
+//   * The sparse row's (k-block, storage-block) list is staged once per tile
+//     into LDS; each k-step resolves its block pointer with one LDS read and a
+//     readfirstlane (wave-uniform -> SGPR buffer descriptor), so there is no
+//     dependent global load on the critical path (the reference's TODO at
+//     dependent_tile_access_iterator.h:146-147).
+//   * Workgroup -> tile mapping is XCD-aware: the 8 XCDs each get a
+//     contiguous run of tiles that share dense panels in their private L2.
+#ifndef SPUTNIK_AMD_BLOCK_GEMM_H_
+#define SPUTNIK_AMD_BLOCK_GEMM_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sputnik_amd {
+
+constexpr int kBlock = 128;        // BCSR block edge (only 128 is supported)
+constexpr int kBM = 128;           // output tile rows = one sparse block-row
+constexpr int kBK = 64;            // k depth of one pipeline stage
+constexpr int kStages = 3;         // LDS ring depth
+constexpr int kIndexChunk = 1024;  // sparse-row entries staged in LDS at once
+constexpr uint32_t kOOB = 0x80000000u;      // buffer offset that reads as 0
+constexpr uint32_t kNumRecords = 0x7fffffffu;
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define SPUTNIK_LDS(p) ((__attribute__((address_space(3))) void *)(p))
+#define SPUTNIK_LDS_S4(p) ((__attribute__((address_space(3))) s16x4 *)(p))
+
+// Kernel arguments (passed by value). Byte strides everywhere.
+struct GemmParams {
+  const char *s_data;          // sparse: block data; SDD: dense A'
+  const int *s_offsets;        // sparse: entry range per row
+  const short *s_indices;      // sparse: k-block per entry
+  const int *s_block_offsets;  // sparse, column order: storage block per entry
+  long long s_ld;              // SDD: row (or k-line) stride of A' in bytes
+  const char *d_data;          // dense operand
+  long long d_ld;              // its row (or k-line) stride in bytes
+  char *c_data;                // output
+  long long c_ld;              // dense output row stride in bytes
+  const short *c_row_indices;  // SDD: block-row of each output block
+  const short *c_indices;      // SDD: block-col of each output block
+  int num_rows;                // sparse: #block-rows of S
+  int num_jtiles;              // sparse: #BN-wide tiles of the dense extent
+  int j_limit;                 // dense extent (elements) of the j dimension
+  int k_limit;                 // SDD: K (elements)
+  int num_tiles;               // grid size
+};
+
+// XOR key of the m/n-contiguous image: spreads the 8 k-rows one
+// ds_read_b64_tr_b16 half-wave touches over 8 distinct 32-byte bank sectors.
+__device__ __forceinline__ int tr_key(int k) {
+  return (k & 3) | (((k >> 3) & 1) << 2);
+}
+// XOR key of the k-contiguous image (128-byte rows of 8 x 16-byte chunks):
+// makes each 16-lane ds_read_b128 group hit 16 distinct 16-byte slots.
+__device__ __forceinline__ int kc_key(int row) { return (row >> 1) & 7; }
+
+template <typename T>
+struct MfmaTraits;
+template <>
+struct MfmaTraits<_Float16> {
+  static __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(
+        __builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+        0);
+  }
+};
+template <>
+struct MfmaTraits<__bf16> {
+  static __device__ __forceinline__ f32x4 mfma(s16x8 a, s16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+        __builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+        0);
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0,
+                                           kNumRecords, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds_dst,
+                                      uint32_t voffset) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SPUTNIK_LDS(lds_dst), 16,
+                                           voffset, 0, 0, 0);
+}
+
+// 16x32 operand fragment from a k-contiguous image [rows][64 k] (128-B rows):
+// lane l gets row (row0 + l%16), k = 32*kk + 8*(l/16) .. +7.
+__device__ __forceinline__ s16x8 read_kc(const char *img, int row0, int kk,
+                                         int lane) {
+  const int row = row0 + (lane & 15);
+  const int c = 4 * kk + (lane >> 4);
+  return *reinterpret_cast<const s16x8 *>(img + row * 128 +
+                                          ((c ^ kc_key(row)) << 4));
+}
+
+// Same fragment from an m/n-contiguous image [64 k][cols] (kRowBytes per
+// k-row) via two transpose reads: lane l gets column (col0 + l%16) of
+// k = 32*kk + 8*(l/16) + {0..3} and then + {4..7}.
+//
+// Issued as inline asm on purpose: hipcc cannot tell a ds_read_tr builtin
+// from the LDS-DMA writes still in flight and puts an s_waitcnt vmcnt(0) in
+// front of it, which would drain the whole prefetch ring every k-step. The
+// caller therefore owns the lgkmcnt wait for these registers (lds_wait).
+template <int kRowBytes>
+__device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
+                                         int lane) {
+  const int q = (lane >> 2) & 3;
+  const int p = lane & 3;
+  const int g = lane >> 4;
+  const int sector = col0 >> 4;
+  s16x4 lo, hi;
+  const int k = 32 * kk + 8 * g + q;
+  const uint32_t addr = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) const char *)(
+          img + k * kRowBytes + ((sector ^ tr_key(k)) << 5) + (p << 3)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(addr));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
+               : "=v"(hi)
+               : "v"(addr), "n"(4 * kRowBytes));
+  s16x8 out;
+  out[0] = lo[0]; out[1] = lo[1]; out[2] = lo[2]; out[3] = lo[3];
+  out[4] = hi[0]; out[5] = hi[1]; out[6] = hi[2]; out[7] = hi[3];
+  return out;
+}
+
+// Waits until at most N LDS operations of this wave are outstanding and
+// makes the fragments read so far visible to the compiler as written here,
+// so no MFMA that consumes them is scheduled above the wait.
+template <int N>
+__device__ __forceinline__ void lds_wait(s16x8 (&a)[4], s16x8 (&b)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(%8)"
+               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]),
+                 "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
+               : "n"(N)
+               : "memory");
+}
+
+// Maps the launch index to a tile index so that each XCD (blocks b and b+8
+// share one) walks a contiguous run of tiles. Bijective for any grid size.
+__device__ __forceinline__ int xcd_tile(int bid, int nwg) {
+  const int xcd = bid & 7;
+  const int q = nwg >> 3;
+  const int r = nwg & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+// kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
+// kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
+// kOutT: write O transposed (DDS).
+template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
+          int kBN>
+__global__ void __launch_bounds__(2 * kBN)
+    block_gemm_kernel(const GemmParams p) {
+  constexpr int kWN = kBN / 64;            // waves along j
+  constexpr int kNW = 2 * kWN;             // waves per workgroup
+  constexpr int kThreads = 64 * kNW;
+  constexpr int kSBytes = kBM * kBK * 2;   // 16 KiB
+  constexpr int kDBytes = kBK * kBN * 2;   // 16 or 32 KiB
+  constexpr int kStageBytes = kSBytes + kDBytes;
+  constexpr int kSInstr = kSBytes / 1024 / kNW;  // DMA instrs / wave / stage
+  constexpr int kDInstr = kDBytes / 1024 / kNW;  // (always 4)
+  constexpr int kGroup = kSInstr + kDInstr;      // vmcnt per stage
+  constexpr int kDRowBytes = kBN * 2;            // D m/n-contiguous row
+  constexpr int kDChunksPerRow = kBN / 8;
+  constexpr int kDRowsPerInstr = 64 / kDChunksPerRow;
+  constexpr int kRingBytes = kStages * kStageBytes;
+  constexpr int kIdxBytes = kSparseOut ? 0 : kIndexChunk * 6;
+  static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
+  static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
+
+  __shared__ __attribute__((aligned(1024))) char lds[kRingBytes + kIdxBytes];
+  short *idx_kc = reinterpret_cast<short *>(lds + kRingBytes);
+  int *idx_blk = reinterpret_cast<int *>(lds + kRingBytes + kIndexChunk * 2);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / kWN;
+  const int wn = wave % kWN;
+
+  // ---- tile decode -------------------------------------------------------
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  int srow, j0, entry0 = 0, entries = 0, nsteps;
+  long long out_block = 0;
+  if constexpr (kSparseOut) {
+    out_block = tile;
+    srow = p.c_row_indices[tile];
+    j0 = p.c_indices[tile] * kBlock;
+    nsteps = (p.k_limit + kBK - 1) / kBK;
+  } else {
+    srow = tile % p.num_rows;
+    j0 = (tile / p.num_rows) * kBN;
+    entry0 = p.s_offsets[srow];
+    entries = p.s_offsets[srow + 1] - entry0;
+    nsteps = 0;
+  }
+
+  // ---- per-lane DMA offsets (relative to each step's tile base) ----------
+  uint32_t s_off[kSInstr], d_off[kDInstr];
+  int s_lk[kSInstr], d_lk[kDInstr];  // k of the lane's chunk (SDD k-mask)
+  const long long s_stride = kSparseOut ? p.s_ld : 256;
+#pragma unroll
+  for (int q = 0; q < kSInstr; ++q) {
+    const int g = wave * kSInstr + q;
+    if constexpr (kSKC) {
+      const int row = 8 * g + (lane >> 3);
+      const int c = (lane & 7) ^ kc_key(row);
+      s_off[q] = (uint32_t)(row * s_stride + c * 16);
+      s_lk[q] = c * 8;
+    } else {
+      const int k = 4 * g + (lane >> 4);
+      const int pc = lane & 15;
+      const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
+      s_off[q] = (uint32_t)(k * s_stride + c * 16);
+      s_lk[q] = k;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kDInstr; ++q) {
+    const int g = wave * kDInstr + q;
+    bool ok;
+    if constexpr (kDKC) {
+      const int j = 8 * g + (lane >> 3);
+      const int c = (lane & 7) ^ kc_key(j);
+      d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
+      d_lk[q] = c * 8;
+      ok = j0 + j < p.j_limit;
+    } else {
+      const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
+      const int pc = lane % kDChunksPerRow;
+      const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
+      d_off[q] = (uint32_t)(k * p.d_ld + c * 16);
+      d_lk[q] = k;
+      ok = j0 + c * 8 < p.j_limit;
+    }
+    if (!ok) d_off[q] = kOOB;
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Issue the DMA of pipeline step `step` into ring slot `slot`.
+  auto issue = [&](int step, int slot) {
+    const char *s_base;
+    const char *d_base;
+    int krem = kBK;  // valid k in this step (SDD tail)
+    if constexpr (kSparseOut) {
+      const long long k0 = (long long)step * kBK;
+      krem = p.k_limit - (int)k0;
+      s_base = kSKC ? p.s_data + (long long)srow * kBM * p.s_ld + k0 * 2
+                    : p.s_data + k0 * p.s_ld + (long long)srow * kBM * 2;
+      d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + k0 * 2
+                    : p.d_data + k0 * p.d_ld + (long long)j0 * 2;
+    } else {
+      const int e = step >> 1;
+      const int h = step & 1;
+      const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
+      const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
+      s_base = p.s_data + (long long)blk * (kBlock * kBlock * 2) +
+               (kSKC ? h * (kBK * 2) : h * (kBK * 256));
+      const long long kg = (long long)kblk * kBlock + h * kBK;
+      d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
+                    : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+    }
+    char *slot_base = lds + slot * kStageBytes;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(s_base);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(d_base);
+#pragma unroll
+    for (int q = 0; q < kSInstr; ++q) {
+      uint32_t off = s_off[q];
+      if constexpr (kSparseOut) off = s_lk[q] < krem ? off : kOOB;
+      dma16(rs, slot_base + (wave * kSInstr + q) * 1024, off);
+    }
+#pragma unroll
+    for (int q = 0; q < kDInstr; ++q) {
+      uint32_t off = d_off[q];
+      if constexpr (kSparseOut) off = d_lk[q] < krem ? off : kOOB;
+      dma16(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024, off);
+    }
+  };
+
+  // Consume ring slot `slot`: 2 x (4 S frags, 4 D frags, 16 MFMAs). The
+  // k=32..63 fragments are read while the k=0..31 MFMAs run.
+  constexpr int kReadsPerHalf = (kSKC ? 4 : 8) + (kDKC ? 4 : 8);
+  // lgkmcnt is a 4-bit field: 15 is the loosest count it can express.
+  constexpr int kWaitHalf = kReadsPerHalf > 15 ? 15 : kReadsPerHalf;
+  auto read_half = [&](const char *simg, const char *dimg, int kk,
+                       s16x8 (&af)[4], s16x8 (&bf)[4]) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      if constexpr (kSKC)
+        af[f] = read_kc(simg, 64 * wm + 16 * f, kk, lane);
+      else
+        af[f] = read_mn<kBM * 2>(simg, 64 * wm + 16 * f, kk, lane);
+      if constexpr (kDKC)
+        bf[f] = read_kc(dimg, 64 * wn + 16 * f, kk, lane);
+      else
+        bf[f] = read_mn<kDRowBytes>(dimg, 64 * wn + 16 * f, kk, lane);
+    }
+  };
+  auto mfma_half = [&](s16x8 (&af)[4], s16x8 (&bf)[4]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        acc[a][b] = MfmaTraits<T>::mfma(af[a], bf[b], acc[a][b]);
+  };
+  auto compute = [&](int slot) {
+    const char *simg = lds + slot * kStageBytes;
+    const char *dimg = simg + kSBytes;
+    s16x8 a0[4], b0[4], a1[4], b1[4];
+    read_half(simg, dimg, 0, a0, b0);
+    read_half(simg, dimg, 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_wait<kWaitHalf>(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_half(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_wait<0>(a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_half(a1, b1);
+  };
+
+  auto pipeline = [&](int steps) {
+    if (steps > 0) issue(0, 0);
+    if (steps > 1) issue(1, 1);
+    int slot = 0;
+    for (int s = 0; s < steps; ++s) {
+      if (s + 1 < steps)
+        wait_vmcnt<kGroup>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (s + 2 < steps) {
+        int nslot = slot + 2;
+        nslot = nslot >= kStages ? nslot - kStages : nslot;
+        issue(s + 2, nslot);
+      }
+      compute(slot);
+      slot = slot + 1 == kStages ? 0 : slot + 1;
+    }
+  };
+
+  if constexpr (kSparseOut) {
+    pipeline(nsteps);
+  } else {
+    const bool col_order = p.s_block_offsets != nullptr;
+    for (int base = 0; base < entries; base += kIndexChunk) {
+      const int n = min(kIndexChunk, entries - base);
+      __syncthreads();  // previous chunk fully consumed (ring and index list)
+      for (int e = tid; e < n; e += kThreads) {
+        const int ge = entry0 + base + e;
+        idx_kc[e] = p.s_indices[ge];
+        idx_blk[e] = col_order ? p.s_block_offsets[ge] : ge;
+      }
+      __syncthreads();
+      pipeline(2 * n);
+    }
+  }
+
+  // ---- epilogue: fp32 -> T, staged through LDS, 16-byte coalesced stores --
+  wait_vmcnt<0>();
+  __syncthreads();
+  constexpr int kOutRows = kOutT ? kBN : kBM;
+  constexpr int kOutCols = kOutT ? kBM : kBN;
+  constexpr int kStLd = kOutCols * 2 + 16;  // padded staging row (bytes)
+  static_assert(kOutRows * kStLd <= kRingBytes, "staging fits in the ring");
+  char *st = lds;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int i = 64 * wm + 16 * a + 4 * (lane >> 4);
+      const int j = 64 * wn + 16 * b + (lane & 15);
+      if constexpr (kOutT) {
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        t4 v;
+        v[0] = (T)acc[a][b][0];
+        v[1] = (T)acc[a][b][1];
+        v[2] = (T)acc[a][b][2];
+        v[3] = (T)acc[a][b][3];
+        *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
+              (T)acc[a][b][r];
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int kChunksPerRow = kOutCols / 8;
+  constexpr int kChunks = kOutRows * kChunksPerRow;
+  for (int id = tid; id < kChunks; id += kThreads) {
+    const int row = id / kChunksPerRow;
+    const int cc = id % kChunksPerRow;
+    const uint4 v = *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
+    char *dst;
+    if constexpr (kSparseOut) {
+      dst = p.c_data + out_block * (kBlock * kBlock * 2) + row * (kBlock * 2) +
+            cc * 16;
+    } else if constexpr (kOutT) {
+      if (j0 + row >= p.j_limit) continue;
+      dst = p.c_data + (long long)(j0 + row) * p.c_ld +
+            ((long long)srow * kBM + cc * 8) * 2;
+    } else {
+      if (j0 + cc * 8 >= p.j_limit) continue;
+      dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
+            (long long)(j0 + cc * 8) * 2;
+    }
+    *reinterpret_cast<uint4 *>(dst) = v;
+  }
+}
+
+// Host-side launch of one instantiation (defined in block_gemm.hip).
+hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
+                           bool out_t, const GemmParams &params,
+                           hipStream_t stream);
+
+}  // namespace sputnik_amd
+
+#endif  // SPUTNIK_AMD_BLOCK_GEMM_H_

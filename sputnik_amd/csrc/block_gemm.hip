@@ -1,0 +1,54 @@
+// sputnik-amd: instantiations of the block-sparse GEMM kernel and the
+// variant dispatch. Replaces the reference's per-variant CUTLASS files
+// (sputnik/block/{dsd,dds,sdd}/cutlass/*_align8.cu) and the first-fit
+// registries (dsd/cutlass/dsd.cu:30-66 and siblings): the variant is a pure
+// function of (product, transposes, dtype), so no registry is needed.
+#include "block_gemm.h"
+
+namespace sputnik_amd {
+namespace {
+
+template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT>
+hipError_t Launch(const GemmParams &p, hipStream_t stream) {
+  if (p.num_tiles <= 0) return hipSuccess;
+  constexpr int kBN = kSparseOut ? 128 : 256;
+  hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, kBN>),
+                     dim3(p.num_tiles), dim3(2 * kBN), 0, stream, p);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t LaunchTyped(bool sparse_out, bool s_kc, bool d_kc, bool out_t,
+                       const GemmParams &p, hipStream_t stream) {
+  const int code = (s_kc ? 4 : 0) | (d_kc ? 2 : 0) | (out_t ? 1 : 0);
+  if (sparse_out) {
+    switch (code & 6) {
+      case 6: return Launch<T, true, true, true, false>(p, stream);   // SDD NT
+      case 4: return Launch<T, true, true, false, false>(p, stream);  // SDD NN
+      case 2: return Launch<T, true, false, true, false>(p, stream);  // SDD TT
+      default: return Launch<T, true, false, false, false>(p, stream);  // TN
+    }
+  }
+  switch (code) {
+    case 4: return Launch<T, false, true, false, false>(p, stream);  // DSD NN
+    case 6: return Launch<T, false, true, true, false>(p, stream);   // DSD NT
+    case 0: return Launch<T, false, false, false, false>(p, stream); // DSD TN
+    case 2: return Launch<T, false, false, true, false>(p, stream);  // DSD TT
+    case 3: return Launch<T, false, false, true, true>(p, stream);   // DDS NN
+    case 7: return Launch<T, false, true, true, true>(p, stream);    // DDS NT
+    case 1: return Launch<T, false, false, false, true>(p, stream);  // DDS TN
+    default: return Launch<T, false, true, false, true>(p, stream);  // DDS TT
+  }
+}
+
+}  // namespace
+
+hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
+                           bool out_t, const GemmParams &params,
+                           hipStream_t stream) {
+  if (dtype == 1)
+    return LaunchTyped<__bf16>(sparse_out, s_kc, d_kc, out_t, params, stream);
+  return LaunchTyped<_Float16>(sparse_out, s_kc, d_kc, out_t, params, stream);
+}
+
+}  // namespace sputnik_amd

@@ -1,0 +1,156 @@
+// sputnik-amd: extern "C" boundary (declared in include/sputnik_amd.h).
+//
+// Each function converts the plain-C descriptors to the C++ ones (identical
+// layout, checked below) and runs the same host path as the C++ API, but
+// returns an error code in every case where the reference would abort.
+#include <cstddef>
+#include <cstring>
+
+#include "api_internal.h"
+#include "sputnik/sputnik.h"
+#include "sputnik_amd.h"
+
+using sputnik::block::BlockMatrix;
+using sputnik::block::BlockSize;
+using sputnik::block::Matrix;
+
+static_assert(sizeof(BlockMatrix) == 88, "BlockMatrix ABI");
+static_assert(sizeof(sputnik_block_matrix_t) == 88, "C BlockMatrix ABI");
+static_assert(offsetof(BlockMatrix, block_size) == 12, "ABI");
+static_assert(offsetof(BlockMatrix, data) == 16, "ABI");
+static_assert(offsetof(BlockMatrix, row_indices) == 64, "ABI");
+static_assert(offsetof(BlockMatrix, bitmask) == 72, "ABI");
+static_assert(offsetof(BlockMatrix, create_metadata) == 80, "ABI");
+static_assert(offsetof(sputnik_block_matrix_t, create_metadata) == 80, "ABI");
+static_assert(offsetof(sputnik_block_matrix_t, row_indices) == 64, "ABI");
+static_assert(sizeof(Matrix) == 16 && sizeof(sputnik_matrix_t) == 16, "ABI");
+static_assert(offsetof(Matrix, data) == 8, "ABI");
+
+namespace {
+
+BlockMatrix ToCpp(const sputnik_block_matrix_t *m) {
+  BlockMatrix out(m->rows, m->cols, static_cast<BlockSize>(m->block_size),
+                  m->nonzeros, m->data, m->offsets, m->indices, m->offsets_t,
+                  m->indices_t, m->block_offsets, m->bitmask);
+  out.row_indices = m->row_indices;
+  out.create_metadata = m->create_metadata != 0;
+  return out;
+}
+
+Matrix ToCpp(const sputnik_matrix_t *m) {
+  return Matrix(m->rows, m->cols, m->data);
+}
+
+int Code(hipError_t launch, int status_code) {
+  return status_code != 0 ? status_code : static_cast<int>(launch);
+}
+
+}  // namespace
+
+
+extern "C" {
+
+int sputnik_dsd(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  const BlockMatrix ca = ToCpp(a);
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunDsd(
+      ca, transpose_a != 0, ToCpp(b), transpose_b != 0, ToCpp(c), dtype,
+      ca.create_metadata, static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_dsd_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunDsd(
+      ToCpp(a), transpose_a != 0, ToCpp(b), transpose_b != 0, ToCpp(c), dtype,
+      false, static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_dds(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  const BlockMatrix cb = ToCpp(b);
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunDds(
+      ToCpp(a), transpose_a != 0, cb, transpose_b != 0, ToCpp(c), dtype,
+      cb.create_metadata, static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_dds_ex(const sputnik_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunDds(
+      ToCpp(a), transpose_a != 0, ToCpp(b), transpose_b != 0, ToCpp(c), dtype,
+      false, static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_sdd(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunSdd(
+      ToCpp(a), transpose_a != 0, ToCpp(b), transpose_b != 0, ToCpp(c), dtype,
+      static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
+                        void *stream) {
+  if (!a || (!row_indices && a->nonzeros > 0)) return hipErrorInvalidValue;
+  return sputnik::block::RowIndices(ToCpp(a), row_indices,
+                                    static_cast<hipStream_t>(stream));
+}
+
+int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream) {
+  if (!a || !a->offsets_t || !a->indices_t || !a->block_offsets)
+    return hipErrorInvalidValue;
+  return sputnik::block::Transpose(ToCpp(a), static_cast<hipStream_t>(stream));
+}
+
+int sputnik_can_implement(int op, const void *a, int transpose_a,
+                          const void *b, int transpose_b, const void *c) {
+  return sputnik_amd::CanImplement(op, a, transpose_a != 0, b,
+                                   transpose_b != 0, c)
+             ? 1
+             : 0;
+}
+
+size_t sputnik_abi_block_matrix_size(void) { return sizeof(BlockMatrix); }
+
+size_t sputnik_abi_block_matrix_offset(int field) {
+  switch (field) {
+    case 0: return offsetof(BlockMatrix, rows);
+    case 1: return offsetof(BlockMatrix, cols);
+    case 2: return offsetof(BlockMatrix, nonzeros);
+    case 3: return offsetof(BlockMatrix, block_size);
+    case 4: return offsetof(BlockMatrix, data);
+    case 5: return offsetof(BlockMatrix, offsets);
+    case 6: return offsetof(BlockMatrix, indices);
+    case 7: return offsetof(BlockMatrix, offsets_t);
+    case 8: return offsetof(BlockMatrix, indices_t);
+    case 9: return offsetof(BlockMatrix, block_offsets);
+    case 10: return offsetof(BlockMatrix, row_indices);
+    case 11: return offsetof(BlockMatrix, bitmask);
+    case 12: return offsetof(BlockMatrix, create_metadata);
+    default: return (size_t)-1;
+  }
+}
+
+size_t sputnik_abi_matrix_size(void) { return sizeof(Matrix); }
+
+const char *sputnik_version(void) { return "sputnik-amd 0.1 (gfx950)"; }
+
+}  // extern "C"

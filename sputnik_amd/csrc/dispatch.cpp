@@ -1,0 +1,370 @@
+// sputnik-amd: host side of the sputnik::block API (C++ overloads) and its
+// C-ABI twin (include/sputnik_amd.h).
+//
+// Replaces, for the hot path:
+//   sputnik/block/dsd/dsd.cu:9-27, dds/dds.cu:7-24, sdd/sdd.cu:7-15
+//     (block-size gate, Matmul/MatmulEx),
+//   sputnik/block/{dsd,dds,sdd}/cutlass/<op>.cu (first-fit registries),
+//   the can_launch_* / launch_* bodies of the 12 *_align8.cu variants
+//     (shape rules, metadata checks, operand bundling),
+//   sputnik/block/row_indices/row_indices.cu:24-36 and
+//   sputnik/block/transpose/transpose.cu:69-125 (entry points).
+//
+// Problem -> kernel mapping (see block_gemm.h). Every product is phrased as
+// O = S * D over 128-row tiles of a "row operand" S:
+//   DSD  C = op(A) op(B):  S = op(A) (sparse), D = op(B), O = C.
+//   DDS  C = op(A) op(B):  S = op(B)^T (sparse), D = op(A)^T, O = C^T.
+//   SDD  C = op(A) op(B):  S = op(A) (dense),  D = op(B), O = C's blocks.
+// A sparse S read in column order (DSD TN/TT, DDS NN/TN) uses the transposed
+// metadata (offsets_t, indices_t, block_offsets), exactly like the reference.
+#include <cstdint>
+
+#include "api_internal.h"
+#include "block_gemm.h"
+#include "metadata.h"
+#include "sputnik/sputnik.h"
+#include "sputnik_amd.h"
+
+namespace sputnik_amd {
+namespace {
+
+using sputnik::block::AsInt;
+using sputnik::block::BlockSize;
+using sputnik::block::MatmulShape;
+using sputnik::block::ValidMatmul;
+
+constexpr long long kMaxLaneOffset = 0x7fffffffLL;  // 31-bit buffer offsets
+
+bool DenseOk(const Matrix &m) {
+  return m.rows >= 0 && m.cols >= 0 &&
+         (m.data != nullptr || (long long)m.rows * m.cols == 0);
+}
+
+bool SparseOk(const BlockMatrix &s) {
+  const int b = AsInt(s.block_size);
+  if (b != 128) return false;
+  if (s.rows < 0 || s.cols < 0 || s.nonzeros < 0) return false;
+  if (s.rows % b != 0 || s.cols % b != 0 || s.nonzeros % (b * b) != 0)
+    return false;
+  if ((s.cols / b) > 32767 || (s.rows / b) > 32767) return false;  // int16
+  if (s.offsets == nullptr) return false;
+  if (s.nonzeros > 0 && (s.data == nullptr || s.indices == nullptr))
+    return false;
+  return true;
+}
+
+// The reference's BlockGemm::can_implement: m, n, k multiples of 8
+// (block_gemm.h:728-745; 8 x fp16 = one 16-byte access).
+bool Aligned8(const MatmulShape &s) {
+  return s.m % 8 == 0 && s.n % 8 == 0 && s.k % 8 == 0 && s.m >= 0 &&
+         s.n >= 0 && s.k >= 0;
+}
+
+// Rows of one DMA tile times the byte stride must fit a 31-bit lane offset.
+bool StrideOk(long long rows_in_tile, long long ld_elems) {
+  return rows_in_tile * ld_elems * 2 <= kMaxLaneOffset;
+}
+
+Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const Matrix &c, GemmParams *p, bool *needs_meta) {
+  if (a.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(a) || !DenseOk(b) || !DenseOk(c)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s)) return Status::kNoKernel;
+  const bool d_kc = tb;  // B^T stored [N][K]: k-contiguous
+  if (!StrideOk(d_kc ? 256 : 64, s.ldb)) return Status::kNoKernel;
+  *needs_meta = ta;
+  if (ta && (a.offsets_t == nullptr || a.indices_t == nullptr ||
+             a.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+
+  *p = GemmParams{};
+  p->s_data = static_cast<const char *>(a.data);
+  p->s_offsets = static_cast<const int *>(ta ? a.offsets_t : a.offsets);
+  p->s_indices = static_cast<const short *>(ta ? a.indices_t : a.indices);
+  p->s_block_offsets =
+      ta ? static_cast<const int *>(a.block_offsets) : nullptr;
+  p->d_data = static_cast<const char *>(b.data);
+  p->d_ld = (long long)s.ldb * 2;
+  p->c_data = static_cast<char *>(c.data);
+  p->c_ld = (long long)s.ldc * 2;
+  p->num_rows = s.m / kBM;
+  p->num_jtiles = (s.n + 255) / 256;
+  p->j_limit = s.n;
+  p->num_tiles = p->num_rows * p->num_jtiles;
+  return Status::kOk;
+}
+
+Status PrepareDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const Matrix &c, GemmParams *p, bool *needs_meta) {
+  if (b.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(b) || !DenseOk(a) || !DenseOk(c)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s)) return Status::kNoKernel;
+  const bool d_kc = !ta;  // op(A)^T rows are A's rows when A is [M][K]
+  if (!StrideOk(d_kc ? 256 : 64, s.lda)) return Status::kNoKernel;
+  // Row n of op(B)^T is column n of B when B is stored [K][N] (tb == false).
+  const bool col_order = !tb;
+  *needs_meta = col_order;
+  if (col_order && (b.offsets_t == nullptr || b.indices_t == nullptr ||
+                    b.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+
+  *p = GemmParams{};
+  p->s_data = static_cast<const char *>(b.data);
+  p->s_offsets = static_cast<const int *>(col_order ? b.offsets_t : b.offsets);
+  p->s_indices =
+      static_cast<const short *>(col_order ? b.indices_t : b.indices);
+  p->s_block_offsets =
+      col_order ? static_cast<const int *>(b.block_offsets) : nullptr;
+  p->d_data = static_cast<const char *>(a.data);
+  p->d_ld = (long long)s.lda * 2;
+  p->c_data = static_cast<char *>(c.data);
+  p->c_ld = (long long)s.ldc * 2;
+  p->num_rows = s.n / kBM;
+  p->num_jtiles = (s.m + 255) / 256;
+  p->j_limit = s.m;
+  p->num_tiles = p->num_rows * p->num_jtiles;
+  return Status::kOk;
+}
+
+Status PrepareSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, GemmParams *p) {
+  if (c.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(c) || !DenseOk(a) || !DenseOk(b)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s)) return Status::kNoKernel;
+  if (!StrideOk(ta ? 64 : 128, s.lda) || !StrideOk(tb ? 128 : 64, s.ldb))
+    return Status::kNoKernel;
+  const int blocks = c.nonzeros / (kBlock * kBlock);
+  if (blocks > 0 && c.row_indices == nullptr)
+    return Status::kMissingRowIndices;
+
+  *p = GemmParams{};
+  p->s_data = static_cast<const char *>(a.data);
+  p->s_ld = (long long)s.lda * 2;
+  p->d_data = static_cast<const char *>(b.data);
+  p->d_ld = (long long)s.ldb * 2;
+  p->c_data = static_cast<char *>(c.data);
+  p->c_row_indices = static_cast<const short *>(c.row_indices);
+  p->c_indices = static_cast<const short *>(c.indices);
+  p->num_rows = s.m / kBM;
+  p->j_limit = s.n;
+  p->k_limit = s.k;
+  p->num_tiles = blocks;
+  return Status::kOk;
+}
+
+hipError_t BuildTransposed(const BlockMatrix &a, hipStream_t stream) {
+  const int b = AsInt(a.block_size);
+  if (b == 0) return hipErrorNotSupported;
+  return LaunchTransposeMetadata(
+      a.rows / b, a.cols / b, static_cast<const int *>(a.offsets),
+      static_cast<const short *>(a.indices), static_cast<int *>(a.offsets_t),
+      static_cast<short *>(a.indices_t), static_cast<int *>(a.block_offsets),
+      stream);
+}
+
+// C++ API convention: abort where the reference aborts.
+hipError_t OrAbort(Status st, const char *op) {
+  switch (st) {
+    case Status::kOk: return hipSuccess;
+    case Status::kNotSupported: return hipErrorNotSupported;
+    case Status::kNoKernel:
+      SPUTNIK_LOG(FATAL) << "No compatible kernel for " << op << " problem.";
+      break;
+    case Status::kMissingMetadata:
+      SPUTNIK_LOG(FATAL) << "Check failed: offsets_t && indices_t && "
+                            "block_offsets (" << op << ")";
+      break;
+    case Status::kMissingRowIndices:
+      SPUTNIK_LOG(FATAL) << "Check failed: c.row_indices (" << op << ")";
+      break;
+  }
+  return hipErrorUnknown;
+}
+
+// C-ABI convention: never abort.
+int AsCode(Status st) {
+  switch (st) {
+    case Status::kOk: return hipSuccess;
+    case Status::kNotSupported: return hipErrorNotSupported;
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// ---- shared entry points -------------------------------------------------
+
+hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const Matrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *st_out) {
+  GemmParams p;
+  bool needs_meta = false;
+  const Status st = PrepareDsd(a, ta, b, tb, c, &p, &needs_meta);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  if (needs_meta && build_meta) {
+    const hipError_t e = BuildTransposed(a, stream);
+    if (e != hipSuccess) return e;
+  }
+  return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
+}
+
+hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const Matrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *st_out) {
+  GemmParams p;
+  bool needs_meta = false;
+  const Status st = PrepareDds(a, ta, b, tb, c, &p, &needs_meta);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  if (needs_meta && build_meta) {
+    const hipError_t e = BuildTransposed(b, stream);
+    if (e != hipSuccess) return e;
+  }
+  return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
+                         /*out_t=*/true, p, stream);
+}
+
+hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, hipStream_t stream,
+                  Status *st_out) {
+  GemmParams p;
+  const Status st = PrepareSdd(a, ta, b, tb, c, &p);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, p,
+                         stream);
+}
+
+}  // namespace sputnik_amd
+
+// ---- C++ API (drop-in for the reference's sputnik::block) ---------------
+
+namespace sputnik {
+namespace block {
+
+using sputnik_amd::Status;
+
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, Matrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e =
+      sputnik_amd::RunDsd(a, transpose_a, b, transpose_b, c, (int)dtype,
+                          a.create_metadata, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "dsd");
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const Matrix b,
+                    bool transpose_b, Matrix c, DataType dtype,
+                    hipStream_t stream) {
+  BlockMatrix acp = a;
+  acp.create_metadata = false;
+  return Matmul(acp, transpose_a, b, transpose_b, c, dtype, stream);
+}
+
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, Matrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const Matrix b,
+                    bool transpose_b, Matrix c, hipStream_t stream) {
+  return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, Matrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e =
+      sputnik_amd::RunDds(a, transpose_a, b, transpose_b, c, (int)dtype,
+                          b.create_metadata, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "dds");
+}
+
+hipError_t MatmulEx(const Matrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, Matrix c, DataType dtype,
+                    hipStream_t stream) {
+  BlockMatrix bcp = b;
+  bcp.create_metadata = false;
+  return Matmul(a, transpose_a, bcp, transpose_b, c, dtype, stream);
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, Matrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t MatmulEx(const Matrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, Matrix c, hipStream_t stream) {
+  return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, BlockMatrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e = sputnik_amd::RunSdd(a, transpose_a, b, transpose_b, c,
+                                           (int)dtype, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "sdd");
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, BlockMatrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t RowIndices(BlockMatrix a, short *row_indices, hipStream_t stream) {
+  if (AsInt(a.block_size) == 0) return hipErrorNotSupported;
+  return sputnik_amd::LaunchRowIndices(a.rows / AsInt(a.block_size),
+                                       static_cast<const int *>(a.offsets),
+                                       row_indices, stream);
+}
+
+hipError_t Transpose(BlockMatrix a, hipStream_t stream) {
+  SPUTNIK_CHECK(a.offsets_t);
+  SPUTNIK_CHECK(a.indices_t);
+  SPUTNIK_CHECK(a.block_offsets);
+  return sputnik_amd::BuildTransposed(a, stream);
+}
+
+}  // namespace block
+}  // namespace sputnik
+
+namespace sputnik_amd {
+
+int StatusCode(Status st) { return AsCode(st); }
+
+// Host-only acceptance test (no launch, no device needed): op 0 = DSD
+// (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block). The C
+// descriptors share the C++ layout (static_asserts in c_api.cpp).
+bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
+                  const void *c) {
+  if (!a || !b || !c) return false;
+  GemmParams p;
+  bool meta = false;
+  Status st = Status::kNoKernel;
+  if (op == 0) {
+    st = PrepareDsd(*static_cast<const BlockMatrix *>(a), ta,
+                    *static_cast<const Matrix *>(b), tb,
+                    *static_cast<const Matrix *>(c), &p, &meta);
+  } else if (op == 1) {
+    st = PrepareDds(*static_cast<const Matrix *>(a), ta,
+                    *static_cast<const BlockMatrix *>(b), tb,
+                    *static_cast<const Matrix *>(c), &p, &meta);
+  } else if (op == 2) {
+    st = PrepareSdd(*static_cast<const Matrix *>(a), ta,
+                    *static_cast<const Matrix *>(b), tb,
+                    *static_cast<const BlockMatrix *>(c), &p);
+  }
+  return st == Status::kOk;
+}
+
+}  // namespace sputnik_amd

@@ -1,0 +1,119 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares,
+and its host-only entry points (ABI layout, acceptance rules) behave like the
+reference. No compute call is made (no GPU here)."""
+
+import ctypes
+import os
+import re
+
+import pytest
+
+import sputnik_amd as sp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_c_symbols():
+    src = open(os.path.join(ROOT, "include", "sputnik_amd.h")).read()
+    return sorted(set(re.findall(r"\b(sputnik_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = sp.lib()
+    names = declared_c_symbols()
+    assert len(names) >= 12
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_cpp_api_symbols_exported():
+    """The C++ overload set of the reference (dsd.h, dds.h, sdd.h,
+    row_indices.h, transpose.h) with hipStream_t in place of cudaStream_t."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", sp.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
+    want = [
+        "_ZN7sputnik5block6MatmulENS0_11BlockMatrixEbNS0_6MatrixEbS2_P12ihipStream_t",
+        "_ZN7sputnik5block8MatmulExENS0_11BlockMatrixEbNS0_6MatrixEbS2_P12ihipStream_t",
+        "_ZN7sputnik5block6MatmulENS0_6MatrixEbNS0_11BlockMatrixEbS1_P12ihipStream_t",
+        "_ZN7sputnik5block8MatmulExENS0_6MatrixEbNS0_11BlockMatrixEbS1_P12ihipStream_t",
+        "_ZN7sputnik5block6MatmulENS0_6MatrixEbS1_bNS0_11BlockMatrixEP12ihipStream_t",
+        "_ZN7sputnik5block10RowIndicesENS0_11BlockMatrixEPsP12ihipStream_t",
+        "_ZN7sputnik5block9TransposeENS0_11BlockMatrixEP12ihipStream_t",
+    ]
+    for w in want:
+        assert w in out, w
+
+
+def test_abi_layout():
+    L = sp.lib()
+    assert L.sputnik_abi_block_matrix_size() == 88
+    assert L.sputnik_abi_matrix_size() == 16
+    expected = [0, 4, 8, 12, 16, 24, 32, 40, 48, 56, 64, 72, 80]
+    assert [L.sputnik_abi_block_matrix_offset(i) for i in range(13)] == expected
+    assert ctypes.sizeof(sp._CBlockMatrix) == 88
+    assert ctypes.sizeof(sp._CMatrix) == 16
+    fields = [f[0] for f in sp._CBlockMatrix._fields_]
+    assert [getattr(sp._CBlockMatrix, f).offset for f in fields] == expected
+
+
+class _T:
+    """Stand-in for a device tensor: only data_ptr() is read by the host
+    checks; nothing is dereferenced."""
+
+    def __init__(self, addr=0x1000):
+        self.addr = addr
+
+    def data_ptr(self):
+        return self.addr
+
+
+def bm(rows, cols, nblocks, block=128, **kw):
+    return sp.BlockMatrix(rows, cols, block, nblocks * block * block, _T(),
+                          _T(), _T(), **kw)
+
+
+def dm(rows, cols):
+    return sp.Matrix(rows, cols, _T())
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_can_implement_dsd(ta, tb):
+    m, k, n = 256, 384, 72
+    a = bm(*((k, m) if ta else (m, k)), 3,
+           **({"offsets_t": _T(), "indices_t": _T(), "block_offsets": _T()}
+              if ta else {}))
+    b = dm(*((n, k) if tb else (k, n)))
+    assert sp.can_implement("dsd", a, ta, b, tb, dm(m, n))
+    assert not sp.can_implement("dsd", a, ta, b, tb, dm(m, n + 8))  # shape
+    assert not sp.can_implement("dsd", a, ta, dm(*((12, k) if tb else (k, 12))),
+                                tb, dm(m, 12))                      # n % 8
+    a64 = bm(*((k, m) if ta else (m, k)), 3, block=64)
+    assert not sp.can_implement("dsd", a64, ta, b, tb, dm(m, n))
+
+
+def test_can_implement_needs_transposed_metadata():
+    a = bm(384, 256, 3)  # stored [K][M]
+    assert not sp.can_implement("dsd", a, True, dm(384, 64), False, dm(256, 64))
+    assert sp.can_implement("dsd", a, False, dm(256, 64), False, dm(384, 64))
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_can_implement_dds_sdd(ta, tb):
+    m, k, n = 40, 256, 384
+    meta = {} if tb else {"offsets_t": _T(), "indices_t": _T(),
+                          "block_offsets": _T()}
+    b = bm(*((n, k) if tb else (k, n)), 2, **meta)
+    a = dm(*((k, m) if ta else (m, k)))
+    assert sp.can_implement("dds", a, ta, b, tb, dm(m, n))
+    m = 256
+    c = bm(m, n, 2, row_indices=_T())
+    a = dm(*((8, m) if ta else (m, 8)))
+    bb = dm(*((n, 8) if tb else (8, n)))
+    assert sp.can_implement("sdd", a, ta, bb, tb, c)
+    c_noidx = bm(m, n, 2)
+    assert not sp.can_implement("sdd", a, ta, bb, tb, c_noidx)
+
+
+def test_version():
+    assert "gfx950" in sp.version()

@@ -1,0 +1,380 @@
+"""GPU parity: the HIP kernels of libsputnik.so (called through the C-ABI via
+sputnik_amd) against the CPU oracle, on the reference's own test problem
+lists (sputnik/block/{dsd,dds,sdd}/*_test.cu) plus edge cases and the
+BASELINE sizes.
+
+Tolerance (tests/helpers.py): |gpu - ref| <= rtol*(|ref| + rms(ref)) with
+rtol = 1e-2 (fp16) / 2e-2 (bf16) against the oracle GEMM of the rounded
+inputs; additionally the reference's criterion, abs 5e-2 against the fp32
+oracle of the un-rounded inputs, on the reference problem lists. Metadata
+builders (Transpose, RowIndices) must be bit-exact.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from sputnik_amd import matrix_utils as mu
+from tests import helpers as H
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected here, skipped: no device
+    pytest.skip("no GPU", allow_module_level=True)
+
+import sputnik_amd as sp  # noqa: E402
+
+sp.lib()  # fail loudly if the native library is missing
+
+
+def _sync():
+    torch.cuda.synchronize()
+
+
+def _problems(op):
+    return [pytest.param(p, id=f"{op}-{i}-m{p['m']}k{p['k']}n{p['n']}"
+                         f"-nz{p['nonzeros']//16384}-{'T' if p['ta'] else 'N'}"
+                         f"{'T' if p['tb'] else 'N'}{'-u' if p['unordered'] else ''}")
+            for i, p in enumerate(H.load_problems(op))]
+
+
+# --------------------------------------------------------------------- DSD --
+
+def run_dsd(p, dtype="f16", seed=0, ex=False):
+    rng = np.random.default_rng(seed)
+    m, k, n, ta, tb = p["m"], p["k"], p["n"], p["ta"], p["tb"]
+    a_rows, a_cols = (k, m) if ta else (m, k)
+    A = H.HostSparse(a_rows, a_cols, p["nonzeros"], rng, dtype,
+                     unordered=p["unordered"])
+    B = H.HostDense(*((n, k) if tb else (k, n)), rng, dtype)
+    C, c_t = H.empty_dense(m, n, dtype)
+    if ta:
+        sp.AllocateTransposeBuffers(A.matrix)
+    if ex:
+        sp.Transpose(A.matrix)
+        sp.MatmulEx(A.matrix, ta, B.matrix, tb, C)
+    else:
+        sp.Matmul(A.matrix, ta, B.matrix, tb, C)
+    _sync()
+    gpu = c_t.float().cpu().numpy()
+    amask = A.mask().T if ta else A.mask()
+    ref = O.gemm(A.dense(), ta, B.values, tb, a_mask=amask,
+                 threads=H.oracle_threads())
+    return gpu, ref, A, B
+
+
+@pytest.mark.parametrize("p", _problems("dsd"))
+def test_dsd_reference_problems(p):
+    gpu, ref, A, B = run_dsd(p)
+    H.assert_close(gpu, ref, "f16", "dsd")
+
+
+@pytest.mark.parametrize("p", _problems("dsd")[::5])
+def test_dsd_reference_criterion_unrounded(p):
+    """abs 5e-2 vs the fp32 oracle of the *un-rounded* inputs, exactly the
+    reference's check (dsd_test.cu:188-193)."""
+    rng = np.random.default_rng(1)
+    gpu, _, A, B = run_dsd(p, seed=1)
+    m, k, n, ta, tb = p["m"], p["k"], p["n"], p["ta"], p["tb"]
+    # Rebuild un-rounded inputs with the same stream: draw again identically.
+    rng = np.random.default_rng(1)
+    a_rows, a_cols = (k, m) if ta else (m, k)
+    b_ = mu.BLOCK
+    nb = p["nonzeros"] // (b_ * b_)
+    off, idx = mu.random_topology(a_rows // b_, a_cols // b_, nb, rng,
+                                  unordered=p["unordered"])
+    vals = mu.random_values((nb, b_, b_), rng)
+    braw = mu.random_values((n, k) if tb else (k, n), rng)
+    dense_a = mu.to_dense(a_rows, a_cols, off, idx, vals)
+    ref = O.gemm(dense_a, ta, braw, tb, threads=H.oracle_threads())
+    assert np.abs(gpu - ref).max() <= H.REF_ABS_TOL
+
+
+@pytest.mark.parametrize("p", _problems("dsd")[24:48:3])
+def test_dsd_bf16(p):
+    gpu, ref, _, _ = run_dsd(p, dtype="bf16")
+    H.assert_close(gpu, ref, "bf16", "dsd-bf16")
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_dsd_matmul_ex(ta, tb):
+    p = dict(m=512, k=768, n=384, nonzeros=10 * 16384, ta=ta, tb=tb,
+             unordered=True)
+    gpu, ref, _, _ = run_dsd(p, ex=True)
+    H.assert_close(gpu, ref, "f16", "dsd-ex")
+
+
+def test_dsd_empty_rows_and_zero_matrix():
+    rng = np.random.default_rng(3)
+    # Block-rows 1 and 3 empty; C must be written with exact zeros there.
+    offsets = np.array([0, 2, 2, 3, 3], dtype=np.int32)
+    indices = np.array([0, 2, 1], dtype=np.int32)
+    A = H.HostSparse(512, 384, 3 * 16384, rng, topology=(offsets, indices))
+    B = H.HostDense(384, 264, rng)
+    C, c_t = H.empty_dense(512, 264)
+    sp.Matmul(A.matrix, False, B.matrix, False, C)
+    _sync()
+    gpu = c_t.float().cpu().numpy()
+    assert (gpu[128:256] == 0).all() and (gpu[384:] == 0).all()
+    ref = O.gemm(A.dense(), False, B.values, False)
+    H.assert_close(gpu, ref, "f16")
+    # No nonzero blocks at all.
+    Z = H.HostSparse(256, 256, 0, rng,
+                     topology=(np.zeros(3, np.int32), np.zeros(0, np.int32)))
+    C2, c2 = H.empty_dense(256, 128)
+    sp.Matmul(Z.matrix, False, H.HostDense(256, 128, rng).matrix, False, C2)
+    _sync()
+    assert (c2.float().cpu().numpy() == 0).all()
+
+
+def test_dsd_deterministic():
+    p = dict(m=1024, k=1024, n=1024, nonzeros=512 * 1024, ta=False, tb=False,
+             unordered=False)
+    rng = np.random.default_rng(5)
+    A = H.HostSparse(1024, 1024, p["nonzeros"], rng)
+    B = H.HostDense(1024, 1024, rng)
+    outs = []
+    for _ in range(2):
+        C, c_t = H.empty_dense(1024, 1024)
+        sp.Matmul(A.matrix, False, B.matrix, False, C)
+        _sync()
+        outs.append(c_t.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("density", [0.1, 0.3, 0.5, 0.9])
+def test_dsd_baseline_config_sampled(density):
+    """BASELINE config 2 (M=K=N=4096) at its four densities: full GPU result,
+    oracle on 3 sampled block-rows (first, middle, last) + row-sum checksum
+    over all rows (linearity: C·1 = A·(B·1))."""
+    rng = np.random.default_rng(7)
+    nz = mu.nonzeros_for_density(4096, 4096, density)
+    A = H.HostSparse(4096, 4096, nz, rng)
+    B = H.HostDense(4096, 4096, rng)
+    C, c_t = H.empty_dense(4096, 4096)
+    sp.Matmul(A.matrix, False, B.matrix, False, C)
+    _sync()
+    gpu = c_t.float().cpu().numpy()
+    dense_a = A.dense()
+    for r in (0, 15, 31):
+        rows = slice(r * 128, (r + 1) * 128)
+        ref = O.gemm(dense_a[rows], False, B.values, False,
+                     a_mask=A.mask()[r:r + 1], threads=H.oracle_threads())
+        H.assert_close(gpu[rows], ref, "f16", f"row-block {r}")
+    ones = B.values.astype(np.float64).sum(axis=1)
+    checksum = dense_a.astype(np.float64) @ ones
+    got = gpu.astype(np.float64).sum(axis=1)
+    scale = np.sqrt(np.mean(checksum ** 2))
+    assert np.abs(got - checksum).max() <= 2e-2 * scale + 1e-2 * np.abs(checksum).max()
+
+
+# --------------------------------------------------------------------- DDS --
+
+def run_dds(p, dtype="f16", seed=0, ex=False):
+    rng = np.random.default_rng(seed)
+    m, k, n, ta, tb = p["m"], p["k"], p["n"], p["ta"], p["tb"]
+    A = H.HostDense(*((k, m) if ta else (m, k)), rng, dtype)
+    b_rows, b_cols = (n, k) if tb else (k, n)
+    B = H.HostSparse(b_rows, b_cols, p["nonzeros"], rng, dtype,
+                     unordered=p["unordered"])
+    C, c_t = H.empty_dense(m, n, dtype)
+    if not tb:
+        sp.AllocateTransposeBuffers(B.matrix)
+    if ex:
+        sp.Transpose(B.matrix)
+        sp.MatmulEx(A.matrix, ta, B.matrix, tb, C)
+    else:
+        sp.Matmul(A.matrix, ta, B.matrix, tb, C)
+    _sync()
+    gpu = c_t.float().cpu().numpy()
+    bmask = B.mask().T if tb else B.mask()
+    ref = O.gemm(A.values, ta, B.dense(), tb, b_mask=bmask,
+                 threads=H.oracle_threads())
+    return gpu, ref
+
+
+@pytest.mark.parametrize("p", _problems("dds"))
+def test_dds_reference_problems(p):
+    gpu, ref = run_dds(p)
+    H.assert_close(gpu, ref, "f16", "dds")
+
+
+@pytest.mark.parametrize("p", _problems("dds")[24:48:3])
+def test_dds_bf16(p):
+    gpu, ref = run_dds(p, dtype="bf16")
+    H.assert_close(gpu, ref, "bf16", "dds-bf16")
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_dds_matmul_ex(ta, tb):
+    p = dict(m=264, k=640, n=512, nonzeros=9 * 16384, ta=ta, tb=tb,
+             unordered=True)
+    gpu, ref = run_dds(p, ex=True)
+    H.assert_close(gpu, ref, "f16", "dds-ex")
+
+
+# --------------------------------------------------------------------- SDD --
+
+def run_sdd(p, dtype="f16", seed=0):
+    rng = np.random.default_rng(seed)
+    m, k, n, ta, tb = p["m"], p["k"], p["n"], p["ta"], p["tb"]
+    A = H.HostDense(*((k, m) if ta else (m, k)), rng, dtype)
+    B = H.HostDense(*((n, k) if tb else (k, n)), rng, dtype)
+    Cs = H.HostSparse(m, n, p["nonzeros"], rng, dtype,
+                      unordered=p["unordered"])
+    Cs.dev_values.fill_(float("nan"))
+    sp.AllocateRowIndicesBuffer(Cs.matrix)
+    sp.RowIndices(Cs.matrix, Cs.matrix.row_indices)
+    sp.Matmul(A.matrix, ta, B.matrix, tb, Cs.matrix)
+    _sync()
+    gpu_blocks = Cs.dev_values.float().cpu().numpy()
+    mask = Cs.mask()
+    ref_dense = O.gemm(A.values, ta, B.values, tb, out_mask=mask,
+                       threads=H.oracle_threads())
+    # Gather the reference at C's nonzero blocks, in storage order.
+    rows = np.repeat(np.arange(len(Cs.offsets) - 1), np.diff(Cs.offsets))
+    b_ = mu.BLOCK
+    ref_blocks = np.stack([ref_dense[r * b_:(r + 1) * b_, c * b_:(c + 1) * b_]
+                           for r, c in zip(rows, Cs.indices)]) \
+        if len(rows) else np.zeros((0, b_, b_), np.float32)
+    return gpu_blocks, ref_blocks
+
+
+@pytest.mark.parametrize("p", _problems("sdd"))
+def test_sdd_reference_problems(p):
+    gpu, ref = run_sdd(p)
+    H.assert_close(gpu, ref, "f16", "sdd")
+
+
+@pytest.mark.parametrize("p", _problems("sdd")[16:40:3])
+def test_sdd_bf16(p):
+    gpu, ref = run_sdd(p, dtype="bf16")
+    H.assert_close(gpu, ref, "bf16", "sdd-bf16")
+
+
+@pytest.mark.parametrize("k", [8, 24, 72, 200])
+def test_sdd_ragged_k(k):
+    """K not a multiple of the 64-deep k-step (reference sdd_test K=8)."""
+    for ta in (False, True):
+        for tb in (False, True):
+            p = dict(m=256, k=k, n=384, nonzeros=4 * 16384, ta=ta, tb=tb,
+                     unordered=False)
+            gpu, ref = run_sdd(p)
+            H.assert_close(gpu, ref, "f16", f"sdd k={k} {ta}{tb}")
+
+
+def test_sdd_dds_pair_config3():
+    """BASELINE config 3 (MegaBlocks fwd/bwd pair at 4096^3, 20%), sampled."""
+    rng = np.random.default_rng(11)
+    nz = mu.nonzeros_for_density(4096, 4096, 0.2)
+    x = H.HostDense(4096, 4096, rng)
+    w = H.HostDense(4096, 4096, rng)
+    Cs = H.HostSparse(4096, 4096, nz, rng)
+    sp.AllocateRowIndicesBuffer(Cs.matrix)
+    sp.RowIndices(Cs.matrix, Cs.matrix.row_indices)
+    sp.Matmul(x.matrix, False, w.matrix, False, Cs.matrix)      # SDD
+    g = H.HostDense(4096, 4096, rng)
+    sp.AllocateTransposeBuffers(Cs.matrix)
+    out, out_t = H.empty_dense(4096, 4096)
+    sp.Matmul(g.matrix, False, Cs.matrix, False, out)            # DDS
+    _sync()
+    blocks = Cs.dev_values.float().cpu().numpy()
+    rows = np.repeat(np.arange(32), np.diff(Cs.offsets))
+    for b in (0, len(rows) // 2, len(rows) - 1):
+        r, c = rows[b], Cs.indices[b]
+        ref = O.gemm(x.values[r * 128:(r + 1) * 128], False,
+                     w.values[:, c * 128:(c + 1) * 128], False)
+        H.assert_close(blocks[b], ref, "f16", f"sdd block {b}")
+    # DDS against the oracle on the SDD output as produced (rounded to fp16).
+    sdd_dense = mu.to_dense(4096, 4096, Cs.offsets, Cs.indices, blocks)
+    for r in (0, 17, 31):
+        ref = O.gemm(g.values[r * 128:(r + 1) * 128], False, sdd_dense, False,
+                     b_mask=Cs.mask(), threads=H.oracle_threads())
+        H.assert_close(out_t[r * 128:(r + 1) * 128].float().cpu().numpy(),
+                       ref, "f16", f"dds row-block {r}")
+
+
+# ------------------------------------------------------------ metadata ----
+
+def _device_topology(offsets, indices, rows_b, cols_b):
+    nb = int(offsets[-1])
+    data = torch.zeros(max(nb, 1) * 128 * 128, dtype=torch.float16,
+                       device="cuda")
+    return sp.BlockMatrix(rows_b * 128, cols_b * 128, 128, nb * 16384, data,
+                          torch.from_numpy(offsets.astype(np.int32)).cuda(),
+                          torch.from_numpy(indices.astype(np.int16)).cuda())
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 6), (1, 1, 1), (32, 32, 512),
+                                   (64, 896, 7168), (1024, 32, 656),
+                                   (5, 9, 0), (16, 300, 2000), (40, 40, 1600)])
+@pytest.mark.parametrize("unordered", [False, True])
+def test_transpose_bit_exact(shape, unordered):
+    rows_b, cols_b, nb = shape
+    rng = np.random.default_rng(rows_b * 1000 + cols_b)
+    off, idx = mu.random_topology(rows_b, cols_b, nb, rng, unordered)
+    a = _device_topology(off, idx, rows_b, cols_b)
+    sp.AllocateTransposeBuffers(a)
+    sp.Transpose(a)
+    _sync()
+    ot, it, bo = O.transpose(off, idx, cols_b)
+    assert np.array_equal(a.offsets_t.cpu().numpy(), ot)
+    assert np.array_equal(a.indices_t.cpu().numpy()[:nb], it)
+    assert np.array_equal(a.block_offsets.cpu().numpy()[:nb], bo)
+
+
+def test_transpose_survey_known_answer():
+    """The vector recorded from the reference's own Transpose."""
+    off = np.array([0, 2, 5, 6], np.int32)
+    idx = np.array([1, 3, 2, 0, 3, 1], np.int32)
+    a = _device_topology(off, idx, 3, 4)
+    sp.AllocateTransposeBuffers(a)
+    sp.Transpose(a)
+    _sync()
+    assert a.offsets_t.cpu().tolist() == [0, 1, 3, 4, 6]
+    assert a.indices_t.cpu().tolist() == [1, 0, 2, 1, 0, 1]
+    assert a.block_offsets.cpu().tolist() == [3, 0, 5, 2, 1, 4]
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 6), (32, 32, 512), (1024, 32, 656),
+                                   (64, 896, 7168), (7, 3, 0)])
+def test_row_indices_bit_exact(shape):
+    rows_b, cols_b, nb = shape
+    rng = np.random.default_rng(nb + 1)
+    off, idx = mu.random_topology(rows_b, cols_b, nb, rng)
+    a = _device_topology(off, idx, rows_b, cols_b)
+    sp.AllocateRowIndicesBuffer(a)
+    sp.RowIndices(a, a.row_indices)
+    _sync()
+    assert np.array_equal(a.row_indices.cpu().numpy()[:nb], O.row_indices(off))
+
+
+# ------------------------------------------------------------- errors -----
+
+def test_errors_returned_not_aborted():
+    rng = np.random.default_rng(0)
+    A = H.HostSparse(256, 256, 2 * 16384, rng)
+    B = H.HostDense(256, 128, rng)
+    C, _ = H.empty_dense(256, 128)
+    # Transposed sparse operand without workspaces (reference aborts).
+    with pytest.raises(sp.SputnikError) as e:
+        sp.Matmul(A.matrix, True, B.matrix, False, C)
+    assert e.value.code == sp.hipErrorInvalidValue
+    # Block size other than 128 -> hipErrorNotSupported (dsd.cu:16).
+    A.matrix.block_size = 64
+    with pytest.raises(sp.SputnikError) as e:
+        sp.Matmul(A.matrix, False, B.matrix, False, C)
+    assert e.value.code == sp.hipErrorNotSupported
+    A.matrix.block_size = 128
+    # Shape mismatch (no compatible kernel in the reference).
+    Cbad, _ = H.empty_dense(256, 136)
+    with pytest.raises(sp.SputnikError):
+        sp.Matmul(A.matrix, False, B.matrix, False, Cbad)
+    # SDD without row indices.
+    Cs = H.HostSparse(256, 128, 16384, rng)
+    with pytest.raises(sp.SputnikError):
+        sp.Matmul(H.HostDense(256, 64, rng).matrix, False,
+                  H.HostDense(64, 128, rng).matrix, False, Cs.matrix)
