@@ -26,7 +26,7 @@ step bench 600 python bench.py --steps 100 --warmup 10; rc=$?
 fatal $rc && exit $rc
 cd /tmp
 step_prof() {
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $GRAFT_REPO_ROOT/$OUT/prof -o run -- \
     python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --sweep "" --no-cpu \
     > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1
 }

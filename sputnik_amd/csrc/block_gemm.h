@@ -48,6 +48,7 @@ constexpr int kBM = 128;           // output tile rows = one sparse block-row
 constexpr int kBK = 64;            // k depth of one pipeline stage
 constexpr int kStages = 3;         // LDS ring depth
 constexpr int kIndexChunk = 1024;  // sparse-row entries staged in LDS at once
+constexpr int kLptRows = 256;      // rank block-rows in-kernel up to this many
 constexpr uint32_t kOOB = 0x80000000u;      // buffer offset that reads as 0
 constexpr uint32_t kNumRecords = 0x7fffffffu;
 
@@ -230,10 +231,36 @@ __global__ void __launch_bounds__(2 * kBN)
     j0 = p.c_indices[tile] * kBlock;
     nsteps = (p.k_limit + kBK - 1) / kBK;
   } else {
-    srow = tile % p.num_rows;
+    // Longest-processing-time order: within each dense panel, tile t takes
+    // the block-row with the t-th most nonzeros (ties by row index), so the
+    // workgroups dispatched last are the shortest and fill the gaps left by
+    // earlier ones. Rows are ranked in LDS by every workgroup (R <= kLptRows;
+    // taller matrices have many more tiles than CUs and keep natural order).
+    const int target = tile % p.num_rows;
     j0 = (tile / p.num_rows) * kBN;
-    entry0 = p.s_offsets[srow];
-    entries = p.s_offsets[srow + 1] - entry0;
+    srow = target;
+    if (p.num_rows <= kLptRows) {
+      int *offs = reinterpret_cast<int *>(lds);
+      int *pick = offs + kLptRows + 1;
+      for (int r = tid; r <= p.num_rows; r += kThreads) offs[r] = p.s_offsets[r];
+      __syncthreads();
+      for (int r = tid; r < p.num_rows; r += kThreads) {
+        const int nr = offs[r + 1] - offs[r];
+        int rank = 0;
+        for (int r2 = 0; r2 < p.num_rows; ++r2) {
+          const int n2 = offs[r2 + 1] - offs[r2];
+          rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
+        }
+        if (rank == target) *pick = r;
+      }
+      __syncthreads();
+      srow = __builtin_amdgcn_readfirstlane(*pick);
+      entry0 = offs[srow];
+      entries = offs[srow + 1] - entry0;
+    } else {
+      entry0 = p.s_offsets[srow];
+      entries = p.s_offsets[srow + 1] - entry0;
+    }
     nsteps = 0;
   }
 
@@ -324,65 +351,91 @@ __global__ void __launch_bounds__(2 * kBN)
     }
   };
 
-  // Consume ring slot `slot`: 2 x (4 S frags, 4 D frags, 16 MFMAs). The
-  // k=32..63 fragments are read while the k=0..31 MFMAs run.
-  constexpr int kReadsPerHalf = (kSKC ? 4 : 8) + (kDKC ? 4 : 8);
-  // lgkmcnt is a 4-bit field: 15 is the loosest count it can express.
-  constexpr int kWaitHalf = kReadsPerHalf > 15 ? 15 : kReadsPerHalf;
-  auto read_half = [&](const char *simg, const char *dimg, int kk,
-                       s16x8 (&af)[4], s16x8 (&bf)[4]) {
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      if constexpr (kSKC)
-        af[f] = read_kc(simg, 64 * wm + 16 * f, kk, lane);
-      else
-        af[f] = read_mn<kBM * 2>(simg, 64 * wm + 16 * f, kk, lane);
-      if constexpr (kDKC)
-        bf[f] = read_kc(dimg, 64 * wn + 16 * f, kk, lane);
-      else
-        bf[f] = read_mn<kDRowBytes>(dimg, 64 * wn + 16 * f, kk, lane);
-    }
+  // Fragment registers of one k-step: [kk][f] for the S (a) and D (b)
+  // operands, kk = k-half 0..31 / 32..63.
+  struct Frags {
+    s16x8 a[2][4];
+    s16x8 b[2][4];
   };
-  auto mfma_half = [&](s16x8 (&af)[4], s16x8 (&bf)[4]) {
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-        acc[a][b] = MfmaTraits<T>::mfma(af[a], bf[b], acc[a][b]);
-  };
-  auto compute = [&](int slot) {
+  auto read_step = [&](int slot, Frags &F) {
     const char *simg = lds + slot * kStageBytes;
     const char *dimg = simg + kSBytes;
-    s16x8 a0[4], b0[4], a1[4], b1[4];
-    read_half(simg, dimg, 0, a0, b0);
-    read_half(simg, dimg, 1, a1, b1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        if constexpr (kSKC)
+          F.a[kk][f] = read_kc(simg, 64 * wm + 16 * f, kk, lane);
+        else
+          F.a[kk][f] = read_mn<kBM * 2>(simg, 64 * wm + 16 * f, kk, lane);
+        if constexpr (kDKC)
+          F.b[kk][f] = read_kc(dimg, 64 * wn + 16 * f, kk, lane);
+        else
+          F.b[kk][f] = read_mn<kDRowBytes>(dimg, 64 * wn + 16 * f, kk, lane);
+      }
+    }
+  };
+  auto wait_step = [&](Frags &F) {
     __builtin_amdgcn_sched_barrier(0);
-    lds_wait<kWaitHalf>(a0, b0);
+    lds_wait<0>(F.a[0], F.b[0]);
+    lds_wait<0>(F.a[1], F.b[1]);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_half(a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    lds_wait<0>(a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_half(a1, b1);
+  };
+  auto mfma_step = [&](Frags &F) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
   };
 
+  // Software pipeline over k-steps. Ring slot of step s is s % 3. At the top
+  // of step s the fragments of s are already in registers (cur); the step
+  //   1. waits for its own DMA of step s+1 (counted vmcnt: s+2 stays in
+  //      flight) and meets the other waves at a raw s_barrier, after which
+  //      step s+1's slot is complete and step s's slot is no longer read;
+  //   2. refills step s's slot with the DMA of step s+3;
+  //   3. issues the LDS reads of step s+1 into `next` and, without waiting for
+  //      them, the 32 MFMAs of step s on `cur`;
+  //   4. waits for `next`.
+  // DMA therefore has two steps of MFMA time to land and the LDS read latency
+  // hides under the MFMAs.
   auto pipeline = [&](int steps) {
-    if (steps > 0) issue(0, 0);
+    if (steps <= 0) return;
+    issue(0, 0);
     if (steps > 1) issue(1, 1);
-    int slot = 0;
-    for (int s = 0; s < steps; ++s) {
-      if (s + 1 < steps)
-        wait_vmcnt<kGroup>();
-      else
-        wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();
-      if (s + 2 < steps) {
-        int nslot = slot + 2;
-        nslot = nslot >= kStages ? nslot - kStages : nslot;
-        issue(s + 2, nslot);
+    if (steps > 2) issue(2, 2);
+    if (steps > 2)
+      wait_vmcnt<2 * kGroup>();
+    else if (steps > 1)
+      wait_vmcnt<kGroup>();
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    Frags f0, f1;
+    read_step(0, f0);
+    wait_step(f0);
+    int slot = 0;  // slot of step s
+    auto body = [&](int s, Frags &cur, Frags &next) {
+      const int nslot = slot + 1 == kStages ? 0 : slot + 1;
+      if (s + 1 < steps) {
+        if (s + 2 < steps)
+          wait_vmcnt<kGroup>();
+        else
+          wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (s + 3 < steps) issue(s + 3, slot);
+        read_step(nslot, next);
       }
-      compute(slot);
-      slot = slot + 1 == kStages ? 0 : slot + 1;
+      mfma_step(cur);
+      if (s + 1 < steps) wait_step(next);
+      slot = nslot;
+    };
+    for (int s = 0; s < steps; s += 2) {
+      body(s, f0, f1);
+      if (s + 1 < steps) body(s + 1, f1, f0);
     }
   };
 

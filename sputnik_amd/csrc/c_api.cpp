@@ -115,8 +115,14 @@ int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
 }
 
 int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream) {
-  if (!a || !a->offsets_t || !a->indices_t || !a->block_offsets)
+  // A matrix without nonzero blocks has empty (possibly null) per-block
+  // workspaces; only offsets_t must exist.
+  if (!a || !a->offsets_t || !a->offsets) return hipErrorInvalidValue;
+  if (a->nonzeros > 0 && (!a->indices_t || !a->block_offsets || !a->indices))
     return hipErrorInvalidValue;
+  if (a->block_size != 128 && a->block_size != 64 && a->block_size != 32 &&
+      a->block_size != 16)
+    return hipErrorNotSupported;
   return sputnik::block::Transpose(ToCpp(a), static_cast<hipStream_t>(stream));
 }
 

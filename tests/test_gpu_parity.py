@@ -49,7 +49,7 @@ def run_dsd(p, dtype="f16", seed=0, ex=False):
                      unordered=p["unordered"])
     B = H.HostDense(*((n, k) if tb else (k, n)), rng, dtype)
     C, c_t = H.empty_dense(m, n, dtype)
-    if ta:
+    if ta or ex:
         sp.AllocateTransposeBuffers(A.matrix)
     if ex:
         sp.Transpose(A.matrix)
@@ -180,7 +180,7 @@ def run_dds(p, dtype="f16", seed=0, ex=False):
     B = H.HostSparse(b_rows, b_cols, p["nonzeros"], rng, dtype,
                      unordered=p["unordered"])
     C, c_t = H.empty_dense(m, n, dtype)
-    if not tb:
+    if not tb or ex:
         sp.AllocateTransposeBuffers(B.matrix)
     if ex:
         sp.Transpose(B.matrix)
