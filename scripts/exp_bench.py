@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of variant libraries (build/exp/*.so) on one
+problem in one process (methodology rule: rounds interleaved, median).
+Usage: exp_bench.py [--density D] [--m M] lib1.so lib2.so ..."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--density", type=float, default=0.5)
+    ap.add_argument("--m", type=int, default=4096)
+    ap.add_argument("--k", type=int, default=4096)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--dtype", default="f16")
+    args = ap.parse_args()
+    import torch
+    import bench
+    torch.cuda.set_device(0)
+    prob = bench.Problem(args.m, args.k, args.n, args.density, args.dtype, 0,
+                         torch.device("cuda", 0))
+    ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
+    stream = torch.cuda.current_stream().cuda_stream
+    fns = []
+    for path in args.libs:
+        L = ctypes.CDLL(os.path.abspath(path))
+        fn = L.sputnik_dsd_ex
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                       ctypes.c_void_p]
+        fn.restype = ctypes.c_int
+        a = (ctypes.byref(ca), 0, ctypes.byref(cb), 0, ctypes.byref(cc),
+             prob.dtype_code, stream)
+        assert fn(*a) == 0, path
+        fns.append((os.path.basename(path), fn, a))
+    times = {n: [] for n, _, _ in fns}
+    for _ in range(3):
+        for n, fn, a in fns:
+            fn(*a)
+    torch.cuda.synchronize()
+    for r in range(args.rounds):
+        for n, fn, a in fns:
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.iters):
+                fn(*a)
+            e.record()
+            torch.cuda.synchronize()
+            times[n].append(s.elapsed_time(e) / args.iters * 1e3)
+    out = {}
+    for n, t in times.items():
+        med = statistics.median(t)
+        out[n] = {"us_median": round(med, 2), "us_min": round(min(t), 2),
+                  "tflops": round(prob.flops / (med * 1e-6) / 1e12, 1)}
+    print(json.dumps({"density": args.density, "m": args.m, "k": args.k,
+                      "n": args.n, "results": out}))
+
+
+if __name__ == "__main__":
+    main()

@@ -26,7 +26,7 @@ from dataclasses import dataclass, field
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsputnik.so")
+LIB_PATH = os.environ.get("SPUTNIK_AMD_LIB") or os.path.join(_HERE, "libsputnik.so")
 
 hipSuccess = 0
 hipErrorInvalidValue = 1

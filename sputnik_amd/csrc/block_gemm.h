@@ -41,12 +41,25 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Ablation switches for performance experiments only (scripts/exp_build.sh);
+// the shipped library is built with SPUTNIK_EXP == 0.
+//   1: skip the MFMAs (keep LDS reads)   2: skip the operand DMA
+//   4: no LPT row order                  8: no XCD-aware tile map
+//  16: per-workgroup s_memtime phase stamps into GemmParams::debug
+// 128: skip the LDS fragment reads (MFMAs run on stale registers)
+// 256: LPT without the snake (every panel in descending order)
+//  64: every DMA re-reads step 0's tiles (cache-resident: isolates the memory
+//      system from the LDS-write / issue cost of the DMA)
+//  32: (with 16) per-step wait accounting: cycles in vmcnt wait, barrier,
+//      issue (DMA + LDS reads + MFMA issue), final lgkmcnt wait
+#ifndef SPUTNIK_EXP
+#define SPUTNIK_EXP 0
+#endif
+
 namespace sputnik_amd {
 
 constexpr int kBlock = 128;        // BCSR block edge (only 128 is supported)
 constexpr int kBM = 128;           // output tile rows = one sparse block-row
-constexpr int kBK = 64;            // k depth of one pipeline stage
-constexpr int kStages = 3;         // LDS ring depth
 constexpr int kIndexChunk = 1024;  // sparse-row entries staged in LDS at once
 constexpr int kLptRows = 256;      // rank block-rows in-kernel up to this many
 constexpr uint32_t kOOB = 0x80000000u;      // buffer offset that reads as 0
@@ -79,6 +92,7 @@ struct GemmParams {
   int j_limit;                 // dense extent (elements) of the j dimension
   int k_limit;                 // SDD: K (elements)
   int num_tiles;               // grid size
+  unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one
@@ -86,9 +100,14 @@ struct GemmParams {
 __device__ __forceinline__ int tr_key(int k) {
   return (k & 3) | (((k >> 3) & 1) << 2);
 }
-// XOR key of the k-contiguous image (128-byte rows of 8 x 16-byte chunks):
-// makes each 16-lane ds_read_b128 group hit 16 distinct 16-byte slots.
-__device__ __forceinline__ int kc_key(int row) { return (row >> 1) & 7; }
+// XOR key of the k-contiguous image (rows of kChunks 16-byte chunks, i.e.
+// 128-byte rows at BK=64, 64-byte rows at BK=32): makes each 16-lane
+// ds_read_b128 group hit 16 distinct 16-byte slots (checked exhaustively for
+// both widths by scripts/lds_banks.py).
+template <int kChunks>
+__device__ __forceinline__ int kc_key(int row) {
+  return (row >> 1) & (kChunks - 1);
+}
 
 template <typename T>
 struct MfmaTraits;
@@ -125,14 +144,15 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds_dst,
                                            voffset, 0, 0, 0);
 }
 
-// 16x32 operand fragment from a k-contiguous image [rows][64 k] (128-B rows):
-// lane l gets row (row0 + l%16), k = 32*kk + 8*(l/16) .. +7.
+// 16x32 operand fragment from a k-contiguous image [rows][BK] (kRowBytes =
+// 2*BK per row): lane l gets row (row0 + l%16), k = 32*kk + 8*(l/16) .. +7.
+template <int kRowBytes>
 __device__ __forceinline__ s16x8 read_kc(const char *img, int row0, int kk,
                                          int lane) {
   const int row = row0 + (lane & 15);
   const int c = 4 * kk + (lane >> 4);
-  return *reinterpret_cast<const s16x8 *>(img + row * 128 +
-                                          ((c ^ kc_key(row)) << 4));
+  return *reinterpret_cast<const s16x8 *>(
+      img + row * kRowBytes + ((c ^ kc_key<kRowBytes / 16>(row)) << 4));
 }
 
 // Same fragment from an m/n-contiguous image [64 k][cols] (kRowBytes per
@@ -142,7 +162,7 @@ __device__ __forceinline__ s16x8 read_kc(const char *img, int row0, int kk,
 // Issued as inline asm on purpose: hipcc cannot tell a ds_read_tr builtin
 // from the LDS-DMA writes still in flight and puts an s_waitcnt vmcnt(0) in
 // front of it, which would drain the whole prefetch ring every k-step. The
-// caller therefore owns the lgkmcnt wait for these registers (lds_wait).
+// caller therefore owns the lgkmcnt wait for these registers (wait_step).
 template <int kRowBytes>
 __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
                                          int lane) {
@@ -165,16 +185,14 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
   return out;
 }
 
-// Waits until at most N LDS operations of this wave are outstanding and
-// makes the fragments read so far visible to the compiler as written here,
-// so no MFMA that consumes them is scheduled above the wait.
-template <int N>
-__device__ __forceinline__ void lds_wait(s16x8 (&a)[4], s16x8 (&b)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(%8)"
-               : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(b[0]),
-                 "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
-               : "n"(N)
-               : "memory");
+// Experiment builds: record (wave 0, lane 0) a per-workgroup timeline.
+// Layout per workgroup: [realtime start, memtime start, memtime prologue end,
+// memtime loop end, memtime end, xcc_id, hw_id, k-steps].
+__device__ __forceinline__ void exp_stamp(unsigned long long *dbg, int slot,
+                                          unsigned long long v) {
+  if constexpr ((SPUTNIK_EXP & 16) != 0) {
+    if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 8 + slot] = v;
+  }
 }
 
 // Maps the launch index to a tile index so that each XCD (blocks b and b+8
@@ -187,29 +205,73 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// Tile configuration. The output tile is 128 x kBN; kWM x kWN waves each own
+// a (128/kWM) x (kBN/kWN) sub-tile of 16x16 MFMA accumulators; kBK is the k
+// depth of one LDS ring slot; kWGs workgroups are meant to share a CU (it
+// sets the register budget through __launch_bounds__ and must match the LDS
+// footprint).
+template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_>
+struct TileConfig {
+  static constexpr int kBN = BN_, kWM = WM_, kWN = WN_, kBK = BK_;
+  static constexpr int kStages = STAGES_, kWGs = WGS_;
+};
+
+// 8 waves, 64x64 each, BK=64, one workgroup per CU (first-generation DSD/DDS).
+using CfgWide = TileConfig<256, 2, 4, 64, 3, 1>;
+// 4 waves, 64x128 each, BK=32, two workgroups per CU: 25% fewer LDS fragment
+// bytes per MFMA and two independent barrier domains per CU.
+using CfgDual = TileConfig<256, 2, 2, 32, 3, 2>;
+// 2 waves of 128x128 (one per SIMD, 512-register budget), BK=32, two
+// workgroups per CU: a third fewer LDS fragment bytes per MFMA than CfgDual.
+using CfgQuad = TileConfig<256, 1, 2, 32, 3, 2>;
+// 128x512 tile, 4 waves of 128x128, BK=32, one workgroup per CU.
+using CfgWide512 = TileConfig<512, 1, 4, 32, 3, 1>;
+// SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
+using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
+
+#ifndef SPUTNIK_SPARSE_CFG
+#define SPUTNIK_SPARSE_CFG CfgDual
+#endif
+using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
+
 // kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
 // kOutT: write O transposed (DDS).
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
-          int kBN>
-__global__ void __launch_bounds__(2 * kBN)
+          class Cfg>
+__global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
+                                  Cfg::kWGs * Cfg::kWM * Cfg::kWN / 4)
     block_gemm_kernel(const GemmParams p) {
-  constexpr int kWN = kBN / 64;            // waves along j
-  constexpr int kNW = 2 * kWN;             // waves per workgroup
+  constexpr int kBN = Cfg::kBN;
+  constexpr int kBK = Cfg::kBK;
+  constexpr int kStages = Cfg::kStages;
+  constexpr int kWN = Cfg::kWN;
+  constexpr int kNW = Cfg::kWM * Cfg::kWN;   // waves per workgroup
+  constexpr int kTM = kBM / Cfg::kWM;        // wave sub-tile rows
+  constexpr int kTN = kBN / Cfg::kWN;        // wave sub-tile cols
+  constexpr int kFM = kTM / 16;              // 16x16 accumulators per wave
+  constexpr int kFN = kTN / 16;
+  constexpr int kKK = kBK / 32;              // MFMA k-steps per slot
   constexpr int kThreads = 64 * kNW;
-  constexpr int kSBytes = kBM * kBK * 2;   // 16 KiB
-  constexpr int kDBytes = kBK * kBN * 2;   // 16 or 32 KiB
+  constexpr int kSBytes = kBM * kBK * 2;
+  constexpr int kDBytes = kBK * kBN * 2;
   constexpr int kStageBytes = kSBytes + kDBytes;
   constexpr int kSInstr = kSBytes / 1024 / kNW;  // DMA instrs / wave / stage
-  constexpr int kDInstr = kDBytes / 1024 / kNW;  // (always 4)
+  constexpr int kDInstr = kDBytes / 1024 / kNW;
   constexpr int kGroup = kSInstr + kDInstr;      // vmcnt per stage
+  constexpr int kKcRow = kBK * 2;                // k-contiguous image row
+  constexpr int kKcChunks = kBK / 8;
+  constexpr int kKcRowsPerInstr = 64 / kKcChunks;
   constexpr int kDRowBytes = kBN * 2;            // D m/n-contiguous row
   constexpr int kDChunksPerRow = kBN / 8;
   constexpr int kDRowsPerInstr = 64 / kDChunksPerRow;
+  constexpr int kStepsPerBlock = kBlock / kBK;
   constexpr int kRingBytes = kStages * kStageBytes;
   constexpr int kIdxBytes = kSparseOut ? 0 : kIndexChunk * 6;
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
+  static_assert(kTM % 16 == 0 && kTN % 16 == 0 && kBK % 32 == 0, "tiles");
+  static_assert(Cfg::kWGs * (kRingBytes + kIdxBytes) <= 163840, "LDS budget");
 
   __shared__ __attribute__((aligned(1024))) char lds[kRingBytes + kIdxBytes];
   short *idx_kc = reinterpret_cast<short *>(lds + kRingBytes);
@@ -220,9 +282,21 @@ __global__ void __launch_bounds__(2 * kBN)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / kWN;
   const int wn = wave % kWN;
+  const int row_w = kTM * wm;  // first row / col of this wave's sub-tile
+  const int col_w = kTN * wn;
 
+  if constexpr ((SPUTNIK_EXP & 16) != 0) {
+    unsigned xcc, hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    exp_stamp(p.debug, 0, __builtin_amdgcn_s_memrealtime());
+    exp_stamp(p.debug, 1, __builtin_amdgcn_s_memtime());
+    exp_stamp(p.debug, 5, xcc);
+    exp_stamp(p.debug, 6, hwid);
+  }
   // ---- tile decode -------------------------------------------------------
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
+                                     : xcd_tile(blockIdx.x, gridDim.x);
   int srow, j0, entry0 = 0, entries = 0, nsteps;
   long long out_block = 0;
   if constexpr (kSparseOut) {
@@ -236,10 +310,38 @@ __global__ void __launch_bounds__(2 * kBN)
     // workgroups dispatched last are the shortest and fill the gaps left by
     // earlier ones. Rows are ranked in LDS by every workgroup (R <= kLptRows;
     // taller matrices have many more tiles than CUs and keep natural order).
-    const int target = tile % p.num_rows;
-    j0 = (tile / p.num_rows) * kBN;
+    // Snake: odd panels run ascending. Two workgroups that share a CU (or
+    // follow each other on it) then pair a long row with a short one.
+    int panel = tile / p.num_rows;
+    int target = tile % p.num_rows;
+    if (Cfg::kWGs > 1 && !(SPUTNIK_EXP & 256) && (panel & 1))
+      target = p.num_rows - 1 - target;
+#if defined(SPUTNIK_XJ) && SPUTNIK_XJ > 0
+    {
+      // Grouped XCD map (experiment): XCD x owns kXJ panels of one panel
+      // group and the rows of one rank class; slots s and s + T/16 (assumed
+      // to share a CU) pair local row q with its complement.
+      constexpr int kXJ = SPUTNIK_XJ;
+      const int R = p.num_rows, J = p.num_jtiles, NT = R * J;
+      const int njg = J / kXJ;
+      if (J % kXJ == 0 && njg > 0 && 8 % njg == 0 && NT % 16 == 0 &&
+          R % (2 * (8 / njg)) == 0 && gridDim.x == (unsigned)NT) {
+        const int nrs = 8 / njg;
+        const int x = blockIdx.x & 7;
+        const int s = blockIdx.x >> 3;
+        const int half = s / (NT / 16);
+        const int c = s % (NT / 16);
+        const int nr = R / nrs;
+        const int q = c / kXJ;
+        const int local = half == 0 ? q : nr - 1 - q;
+        target = local * nrs + x / njg;
+        panel = (x % njg) * kXJ + c % kXJ;
+      }
+    }
+#endif
+    j0 = panel * kBN;
     srow = target;
-    if (p.num_rows <= kLptRows) {
+    if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
       int *offs = reinterpret_cast<int *>(lds);
       int *pick = offs + kLptRows + 1;
       for (int r = tid; r <= p.num_rows; r += kThreads) offs[r] = p.s_offsets[r];
@@ -272,8 +374,8 @@ __global__ void __launch_bounds__(2 * kBN)
   for (int q = 0; q < kSInstr; ++q) {
     const int g = wave * kSInstr + q;
     if constexpr (kSKC) {
-      const int row = 8 * g + (lane >> 3);
-      const int c = (lane & 7) ^ kc_key(row);
+      const int row = kKcRowsPerInstr * g + lane / kKcChunks;
+      const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(row);
       s_off[q] = (uint32_t)(row * s_stride + c * 16);
       s_lk[q] = c * 8;
     } else {
@@ -289,8 +391,8 @@ __global__ void __launch_bounds__(2 * kBN)
     const int g = wave * kDInstr + q;
     bool ok;
     if constexpr (kDKC) {
-      const int j = 8 * g + (lane >> 3);
-      const int c = (lane & 7) ^ kc_key(j);
+      const int j = kKcRowsPerInstr * g + lane / kKcChunks;
+      const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(j);
       d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
       d_lk[q] = c * 8;
       ok = j0 + j < p.j_limit;
@@ -305,14 +407,16 @@ __global__ void __launch_bounds__(2 * kBN)
     if (!ok) d_off[q] = kOOB;
   }
 
-  f32x4 acc[4][4];
+  f32x4 acc[kFM][kFN];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < kFM; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // Issue the DMA of pipeline step `step` into ring slot `slot`.
   auto issue = [&](int step, int slot) {
+    if constexpr ((SPUTNIK_EXP & 2) != 0) return;
+    if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
     const char *s_base;
     const char *d_base;
     int krem = kBK;  // valid k in this step (SDD tail)
@@ -324,8 +428,8 @@ __global__ void __launch_bounds__(2 * kBN)
       d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + k0 * 2
                     : p.d_data + k0 * p.d_ld + (long long)j0 * 2;
     } else {
-      const int e = step >> 1;
-      const int h = step & 1;
+      const int e = step / kStepsPerBlock;
+      const int h = step % kStepsPerBlock;
       const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
       const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
       s_base = p.s_data + (long long)blk * (kBlock * kBlock * 2) +
@@ -354,40 +458,60 @@ __global__ void __launch_bounds__(2 * kBN)
   // Fragment registers of one k-step: [kk][f] for the S (a) and D (b)
   // operands, kk = k-half 0..31 / 32..63.
   struct Frags {
-    s16x8 a[2][4];
-    s16x8 b[2][4];
+    s16x8 a[kKK][kFM];
+    s16x8 b[kKK][kFN];
   };
   auto read_step = [&](int slot, Frags &F) {
+    if constexpr ((SPUTNIK_EXP & 128) != 0) return;
     const char *simg = lds + slot * kStageBytes;
     const char *dimg = simg + kSBytes;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < kKK; ++kk) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = 0; f < kFM; ++f) {
         if constexpr (kSKC)
-          F.a[kk][f] = read_kc(simg, 64 * wm + 16 * f, kk, lane);
+          F.a[kk][f] = read_kc<kKcRow>(simg, row_w + 16 * f, kk, lane);
         else
-          F.a[kk][f] = read_mn<kBM * 2>(simg, 64 * wm + 16 * f, kk, lane);
+          F.a[kk][f] = read_mn<kBM * 2>(simg, row_w + 16 * f, kk, lane);
+      }
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) {
         if constexpr (kDKC)
-          F.b[kk][f] = read_kc(dimg, 64 * wn + 16 * f, kk, lane);
+          F.b[kk][f] = read_kc<kKcRow>(dimg, col_w + 16 * f, kk, lane);
         else
-          F.b[kk][f] = read_mn<kDRowBytes>(dimg, 64 * wn + 16 * f, kk, lane);
+          F.b[kk][f] = read_mn<kDRowBytes>(dimg, col_w + 16 * f, kk, lane);
       }
     }
   };
   auto wait_step = [&](Frags &F) {
     __builtin_amdgcn_sched_barrier(0);
-    lds_wait<0>(F.a[0], F.b[0]);
-    lds_wait<0>(F.a[1], F.b[1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int kk = 0; kk < kKK; ++kk) {
+#pragma unroll
+      for (int f = 0; f < kFM; ++f) asm volatile("" : "+v"(F.a[kk][f]));
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) asm volatile("" : "+v"(F.b[kk][f]));
+    }
     __builtin_amdgcn_sched_barrier(0);
   };
   auto mfma_step = [&](Frags &F) {
+    if constexpr ((SPUTNIK_EXP & 1) != 0) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < kKK; ++kk) {
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < kFM; ++a) asm volatile("" ::"v"(F.a[kk][a]));
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < kFN; ++b) asm volatile("" ::"v"(F.b[kk][b]));
+      }
+      return;
+    }
+#pragma unroll
+    for (int kk = 0; kk < kKK; ++kk)
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b)
           acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
   };
 
@@ -402,6 +526,7 @@ __global__ void __launch_bounds__(2 * kBN)
   //   4. waits for `next`.
   // DMA therefore has two steps of MFMA time to land and the LDS read latency
   // hides under the MFMAs.
+  unsigned long long acct[4] = {0, 0, 0, 0};
   auto pipeline = [&](int steps) {
     if (steps <= 0) return;
     issue(0, 0);
@@ -420,17 +545,31 @@ __global__ void __launch_bounds__(2 * kBN)
     int slot = 0;  // slot of step s
     auto body = [&](int s, Frags &cur, Frags &next) {
       const int nslot = slot + 1 == kStages ? 0 : slot + 1;
+      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+      if constexpr ((SPUTNIK_EXP & 32) != 0) t0 = __builtin_amdgcn_s_memtime();
       if (s + 1 < steps) {
         if (s + 2 < steps)
           wait_vmcnt<kGroup>();
         else
           wait_vmcnt<0>();
+        if constexpr ((SPUTNIK_EXP & 32) != 0) t1 = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_barrier();
+        if constexpr ((SPUTNIK_EXP & 32) != 0) t2 = __builtin_amdgcn_s_memtime();
         if (s + 3 < steps) issue(s + 3, slot);
         read_step(nslot, next);
       }
       mfma_step(cur);
+      if constexpr ((SPUTNIK_EXP & 32) != 0) t3 = __builtin_amdgcn_s_memtime();
       if (s + 1 < steps) wait_step(next);
+      if constexpr ((SPUTNIK_EXP & 32) != 0) {
+        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+        if (s + 1 < steps) {
+          acct[0] += t1 - t0;
+          acct[1] += t2 - t1;
+          acct[2] += t3 - t2;
+          acct[3] += t4 - t3;
+        }
+      }
       slot = nslot;
     };
     for (int s = 0; s < steps; s += 2) {
@@ -439,9 +578,12 @@ __global__ void __launch_bounds__(2 * kBN)
     }
   };
 
+  exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
   if constexpr (kSparseOut) {
+    exp_stamp(p.debug, 7, nsteps);
     pipeline(nsteps);
   } else {
+    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
     const bool col_order = p.s_block_offsets != nullptr;
     for (int base = 0; base < entries; base += kIndexChunk) {
       const int n = min(kIndexChunk, entries - base);
@@ -452,61 +594,88 @@ __global__ void __launch_bounds__(2 * kBN)
         idx_blk[e] = col_order ? p.s_block_offsets[ge] : ge;
       }
       __syncthreads();
-      pipeline(2 * n);
+      pipeline(kStepsPerBlock * n);
     }
   }
 
   // ---- epilogue: fp32 -> T, staged through LDS, 16-byte coalesced stores --
   wait_vmcnt<0>();
+  exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
   __syncthreads();
-  constexpr int kOutRows = kOutT ? kBN : kBM;
-  constexpr int kOutCols = kOutT ? kBM : kBN;
+  // The tile is staged in kPasses slices of kPassJ dense columns (j) when
+  // the whole tile does not fit in the ring (128 x 512 tiles).
+  constexpr int kStLdNT = kBN * 2 + 16;  // straight staging row: j-contiguous
+  constexpr int kStLdT = kBM * 2 + 16;   // transposed staging row
+  constexpr int kPasses =
+      kOutT ? ((kBN * kStLdT + kRingBytes - 1) / kRingBytes)
+            : ((kBM * kStLdNT + kRingBytes - 1) / kRingBytes);
+  constexpr int kPassJ = kBN / kPasses;
+  static_assert(kPassJ % 16 == 0 && kPassJ * kPasses == kBN, "passes");
+  constexpr int kOutRows = kOutT ? kPassJ : kBM;  // staging rows per pass
+  constexpr int kOutCols = kOutT ? kBM : kPassJ;
   constexpr int kStLd = kOutCols * 2 + 16;  // padded staging row (bytes)
   static_assert(kOutRows * kStLd <= kRingBytes, "staging fits in the ring");
   char *st = lds;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int pass = 0; pass < kPasses; ++pass) {
+    const int jp0 = pass * kPassJ;
+    if (pass > 0) __syncthreads();  // previous slice fully stored
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int i = 64 * wm + 16 * a + 4 * (lane >> 4);
-      const int j = 64 * wn + 16 * b + (lane & 15);
-      if constexpr (kOutT) {
-        typedef T t4 __attribute__((ext_vector_type(4)));
-        t4 v;
-        v[0] = (T)acc[a][b][0];
-        v[1] = (T)acc[a][b][1];
-        v[2] = (T)acc[a][b][2];
-        v[3] = (T)acc[a][b][3];
-        *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
-      } else {
+    for (int a = 0; a < kFM; ++a) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
-              (T)acc[a][b][r];
+      for (int b = 0; b < kFN; ++b) {
+        const int jb = col_w + 16 * b;  // wave-uniform
+        if (jb < jp0 || jb >= jp0 + kPassJ) continue;
+        const int i = row_w + 16 * a + 4 * (lane >> 4);
+        const int j = jb - jp0 + (lane & 15);
+        if constexpr (kOutT) {
+          typedef T t4 __attribute__((ext_vector_type(4)));
+          t4 v;
+          v[0] = (T)acc[a][b][0];
+          v[1] = (T)acc[a][b][1];
+          v[2] = (T)acc[a][b][2];
+          v[3] = (T)acc[a][b][3];
+          *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
+                (T)acc[a][b][r];
+        }
       }
     }
-  }
-  __syncthreads();
-  constexpr int kChunksPerRow = kOutCols / 8;
-  constexpr int kChunks = kOutRows * kChunksPerRow;
-  for (int id = tid; id < kChunks; id += kThreads) {
-    const int row = id / kChunksPerRow;
-    const int cc = id % kChunksPerRow;
-    const uint4 v = *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
-    char *dst;
-    if constexpr (kSparseOut) {
-      dst = p.c_data + out_block * (kBlock * kBlock * 2) + row * (kBlock * 2) +
-            cc * 16;
-    } else if constexpr (kOutT) {
-      if (j0 + row >= p.j_limit) continue;
-      dst = p.c_data + (long long)(j0 + row) * p.c_ld +
-            ((long long)srow * kBM + cc * 8) * 2;
-    } else {
-      if (j0 + cc * 8 >= p.j_limit) continue;
-      dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
-            (long long)(j0 + cc * 8) * 2;
+    __syncthreads();
+    constexpr int kChunksPerRow = kOutCols / 8;
+    constexpr int kChunks = kOutRows * kChunksPerRow;
+    for (int id = tid; id < kChunks; id += kThreads) {
+      const int row = id / kChunksPerRow;
+      const int cc = id % kChunksPerRow;
+      const uint4 v =
+          *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
+      char *dst;
+      if constexpr (kSparseOut) {
+        dst = p.c_data + out_block * (kBlock * kBlock * 2) +
+              row * (kBlock * 2) + cc * 16;
+      } else if constexpr (kOutT) {
+        const int jrow = j0 + jp0 + row;
+        if (jrow >= p.j_limit) continue;
+        dst = p.c_data + (long long)jrow * p.c_ld +
+              ((long long)srow * kBM + cc * 8) * 2;
+      } else {
+        const int jcol = j0 + jp0 + cc * 8;
+        if (jcol >= p.j_limit) continue;
+        dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
+              (long long)jcol * 2;
+      }
+      *reinterpret_cast<uint4 *>(dst) = v;
     }
-    *reinterpret_cast<uint4 *>(dst) = v;
+  }
+  exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
+  if constexpr ((SPUTNIK_EXP & 32) != 0) {
+    // Overwrite the realtime / id slots with the wait accounting.
+    exp_stamp(p.debug, 0, acct[0]);
+    exp_stamp(p.debug, 5, acct[1]);
+    exp_stamp(p.debug, 6, acct[2] | (acct[3] << 32));
   }
 }
 

@@ -3,6 +3,8 @@
 // (sputnik/block/{dsd,dds,sdd}/cutlass/*_align8.cu) and the first-fit
 // registries (dsd/cutlass/dsd.cu:30-66 and siblings): the variant is a pure
 // function of (product, transposes, dtype), so no registry is needed.
+#include <type_traits>
+
 #include "block_gemm.h"
 
 namespace sputnik_amd {
@@ -11,9 +13,11 @@ namespace {
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT>
 hipError_t Launch(const GemmParams &p, hipStream_t stream) {
   if (p.num_tiles <= 0) return hipSuccess;
-  constexpr int kBN = kSparseOut ? 128 : 256;
-  hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, kBN>),
-                     dim3(p.num_tiles), dim3(2 * kBN), 0, stream, p);
+  using Cfg = typename std::conditional<kSparseOut, CfgBlock,
+                                        CfgSparse>::type;
+  hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, Cfg>),
+                     dim3(p.num_tiles), dim3(64 * Cfg::kWM * Cfg::kWN), 0,
+                     stream, p);
   return hipGetLastError();
 }
 

@@ -26,6 +26,10 @@
 #include "sputnik_amd.h"
 
 namespace sputnik_amd {
+
+// Experiment builds (SPUTNIK_EXP & 16) copy this into GemmParams::debug.
+static unsigned long long *g_debug = nullptr;
+
 namespace {
 
 using sputnik::block::AsInt;
@@ -90,7 +94,7 @@ Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   p->c_data = static_cast<char *>(c.data);
   p->c_ld = (long long)s.ldc * 2;
   p->num_rows = s.m / kBM;
-  p->num_jtiles = (s.n + 255) / 256;
+  p->num_jtiles = (s.n + CfgSparse::kBN - 1) / CfgSparse::kBN;
   p->j_limit = s.n;
   p->num_tiles = p->num_rows * p->num_jtiles;
   return Status::kOk;
@@ -124,7 +128,7 @@ Status PrepareDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   p->c_data = static_cast<char *>(c.data);
   p->c_ld = (long long)s.ldc * 2;
   p->num_rows = s.n / kBM;
-  p->num_jtiles = (s.m + 255) / 256;
+  p->num_jtiles = (s.m + CfgSparse::kBN - 1) / CfgSparse::kBN;
   p->j_limit = s.m;
   p->num_tiles = p->num_rows * p->num_jtiles;
   return Status::kOk;
@@ -212,6 +216,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     const hipError_t e = BuildTransposed(a, stream);
     if (e != hipSuccess) return e;
   }
+  p.debug = g_debug;
   return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
 }
 
@@ -372,3 +377,9 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 }
 
 }  // namespace sputnik_amd
+
+// Experiment hook (not part of include/sputnik_amd.h): phase-stamp buffer
+// for SPUTNIK_EXP & 16 builds; 8 x u64 per workgroup.
+extern "C" void sputnik_exp_set_debug(void *buffer) {
+  sputnik_amd::g_debug = static_cast<unsigned long long *>(buffer);
+}

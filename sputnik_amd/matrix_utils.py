@@ -119,3 +119,13 @@ def shard_rows_by_nnz(offsets: np.ndarray, parts: int):
         bounds.append(r)
     bounds.append(block_rows)
     return [(bounds[i], bounds[i + 1]) for i in range(parts)]
+
+
+def slice_block_rows(offsets, indices, values, r0: int, r1: int):
+    """Rebase block-rows [r0, r1) of a BCSR matrix into a standalone panel:
+    offsets[r0:r1+1] - offsets[r0], with the matching indices / block values
+    (SURVEY §8e). `values` is indexed by block (shape [nb, b, b] or any array
+    whose first axis is the block)."""
+    offsets = np.asarray(offsets)
+    o0, o1 = int(offsets[r0]), int(offsets[r1])
+    return (offsets[r0:r1 + 1] - o0).astype(np.int32), indices[o0:o1], values[o0:o1]
