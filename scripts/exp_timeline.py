@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--density", type=float, default=0.5)
     ap.add_argument("--m", type=int, default=4096)
     ap.add_argument("--acct", action="store_true")
+    ap.add_argument("--skacct", action="store_true")
     args = ap.parse_args()
     import torch
     import bench
@@ -27,7 +28,7 @@ def main():
                          torch.device("cuda", 0))
     L = ctypes.CDLL(os.path.abspath(args.lib))
     L.sputnik_exp_set_debug.argtypes = [ctypes.c_void_p]
-    tiles = (args.m // 128) * 16
+    tiles = max((args.m // 128) * 16, 4096)
     dbg = torch.zeros(tiles * 8, dtype=torch.int64, device="cuda")
     L.sputnik_exp_set_debug(ctypes.c_void_p(dbg.data_ptr()))
     ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
@@ -39,6 +40,8 @@ def main():
         assert fn(ctypes.byref(ca), 0, ctypes.byref(cb), 0, ctypes.byref(cc), 0, stream) == 0
     torch.cuda.synchronize()
     d = dbg.cpu().numpy().reshape(tiles, 8).astype(np.int64)
+    d = d[d[:, 4] != 0]
+    tiles = len(d)
     rt0 = d[:, 0] - d[:, 0].min()
     pro = d[:, 2] - d[:, 1]
     loop = d[:, 3] - d[:, 2]
@@ -64,6 +67,15 @@ def main():
     A = np.vstack([steps, np.ones_like(steps)]).T.astype(float)
     slope, icpt = np.linalg.lstsq(A, loop.astype(float), rcond=None)[0]
     res["loop_fit"] = {"cycles_per_step": round(slope, 1), "intercept": round(icpt, 1)}
+    if args.skacct:
+        res["sk_cycles_median"] = {
+            "pipeline": int(np.median(d[:, 0])), "publish": int(np.median(d[:, 5])),
+            "collect": int(np.median(d[:, 6])), "write": int(np.median(d[:, 7]))}
+        res["sk_cycles_max"] = {
+            "pipeline": int(d[:, 0].max()), "publish": int(d[:, 5].max()),
+            "collect": int(d[:, 6].max()), "write": int(d[:, 7].max())}
+        for k in ("start_skew_us", "wg_start_rt_us_pct", "distinct_cu", "steps", "cycles_per_step", "loop_fit"):
+            res.pop(k, None)
     if args.acct:
         vm = d[:, 0]; bar = d[:, 5]; iss = d[:, 6] & 0xFFFFFFFF; lg = d[:, 6] >> 32
         st = np.maximum(steps, 1)

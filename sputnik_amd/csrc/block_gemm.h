@@ -46,12 +46,10 @@
 //   1: skip the MFMAs (keep LDS reads)   2: skip the operand DMA
 //   4: no LPT row order                  8: no XCD-aware tile map
 //  16: per-workgroup s_memtime phase stamps into GemmParams::debug
-// 128: skip the LDS fragment reads (MFMAs run on stale registers)
-// 256: LPT without the snake (every panel in descending order)
-//  64: every DMA re-reads step 0's tiles (cache-resident: isolates the memory
-//      system from the LDS-write / issue cost of the DMA)
-//  32: (with 16) per-step wait accounting: cycles in vmcnt wait, barrier,
-//      issue (DMA + LDS reads + MFMA issue), final lgkmcnt wait
+//  32: (with 16, stream-K) cycles spent in pipeline / publish / collect /
+//      write+tile lookup, into debug slots 0, 5, 6, 7
+//  64: every DMA re-reads the first step's tiles (cache-resident: isolates
+//      the memory system from the LDS-write / issue cost of the DMA)
 #ifndef SPUTNIK_EXP
 #define SPUTNIK_EXP 0
 #endif
@@ -91,7 +89,14 @@ struct GemmParams {
   int num_jtiles;              // sparse: #BN-wide tiles of the dense extent
   int j_limit;                 // dense extent (elements) of the j dimension
   int k_limit;                 // SDD: K (elements)
-  int num_tiles;               // grid size
+  int num_tiles;               // output tiles (one-tile-per-workgroup grid)
+  // Stream-K (sparse-row products): grid = sk_wgs persistent workgroups that
+  // split the k-steps of all tiles evenly; tiles cut between workgroups are
+  // summed through fp32 partials (one slot per workgroup) and flags.
+  float *sk_partials;          // sk_wgs x (128 x BN) fp32
+  unsigned *sk_flags;          // sk_wgs, compared against sk_epoch
+  unsigned sk_epoch;           // per-launch tag (flags need no reset)
+  int sk_wgs;
   unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
 };
 
@@ -219,12 +224,13 @@ struct TileConfig {
 // 8 waves, 64x64 each, BK=64, one workgroup per CU (first-generation DSD/DDS).
 using CfgWide = TileConfig<256, 2, 4, 64, 3, 1>;
 // 4 waves, 64x128 each, BK=32, two workgroups per CU: 25% fewer LDS fragment
-// bytes per MFMA and two independent barrier domains per CU.
+// bytes per MFMA than CfgWide and two independent barrier domains per CU.
 using CfgDual = TileConfig<256, 2, 2, 32, 3, 2>;
 // 2 waves of 128x128 (one per SIMD, 512-register budget), BK=32, two
-// workgroups per CU: a third fewer LDS fragment bytes per MFMA than CfgDual.
+// workgroups per CU (measured slower than CfgDual: DESIGN.md §10).
 using CfgQuad = TileConfig<256, 1, 2, 32, 3, 2>;
-// 128x512 tile, 4 waves of 128x128, BK=32, one workgroup per CU.
+// 128x512 tile, 4 waves of 128x128, BK=32, one workgroup per CU (measured
+// slower than CfgDual: DESIGN.md §10).
 using CfgWide512 = TileConfig<512, 1, 4, 32, 3, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
@@ -234,14 +240,20 @@ using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
 
+// Bounded spin for the stream-K hand-off (about 0.1 s): a launch can never
+// hang on a missing partial; the tile is then finished without it.
+constexpr int kSpinLimit = 1 << 22;
+
 // kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
 // kOutT: write O transposed (DDS).
+// kStreamK: persistent stream-K decomposition (sparse-row products only).
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
-          class Cfg>
+          class Cfg, bool kStreamK>
 __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                                   Cfg::kWGs * Cfg::kWM * Cfg::kWN / 4)
     block_gemm_kernel(const GemmParams p) {
+  static_assert(!(kStreamK && kSparseOut), "stream-K is for DSD/DDS");
   constexpr int kBN = Cfg::kBN;
   constexpr int kBK = Cfg::kBK;
   constexpr int kStages = Cfg::kStages;
@@ -267,15 +279,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr int kDRowsPerInstr = 64 / kDChunksPerRow;
   constexpr int kStepsPerBlock = kBlock / kBK;
   constexpr int kRingBytes = kStages * kStageBytes;
-  constexpr int kIdxBytes = kSparseOut ? 0 : kIndexChunk * 6;
+  constexpr int kIdxBytes = kSparseOut ? 16 : kIndexChunk * 6 + 16;
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
   static_assert(kTM % 16 == 0 && kTN % 16 == 0 && kBK % 32 == 0, "tiles");
   static_assert(Cfg::kWGs * (kRingBytes + kIdxBytes) <= 163840, "LDS budget");
 
+  // One LDS array (a second __shared__ object can make hipcc drain the DMA
+  // ring before every ds_read): [ring | idx_kc | idx_blk | 4 scratch ints].
   __shared__ __attribute__((aligned(1024))) char lds[kRingBytes + kIdxBytes];
   short *idx_kc = reinterpret_cast<short *>(lds + kRingBytes);
   int *idx_blk = reinterpret_cast<int *>(lds + kRingBytes + kIndexChunk * 2);
+  int *scratch = reinterpret_cast<int *>(lds + kRingBytes + kIdxBytes - 16);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -293,77 +308,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     exp_stamp(p.debug, 1, __builtin_amdgcn_s_memtime());
     exp_stamp(p.debug, 5, xcc);
     exp_stamp(p.debug, 6, hwid);
-  }
-  // ---- tile decode -------------------------------------------------------
-  const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
-                                     : xcd_tile(blockIdx.x, gridDim.x);
-  int srow, j0, entry0 = 0, entries = 0, nsteps;
-  long long out_block = 0;
-  if constexpr (kSparseOut) {
-    out_block = tile;
-    srow = p.c_row_indices[tile];
-    j0 = p.c_indices[tile] * kBlock;
-    nsteps = (p.k_limit + kBK - 1) / kBK;
-  } else {
-    // Longest-processing-time order: within each dense panel, tile t takes
-    // the block-row with the t-th most nonzeros (ties by row index), so the
-    // workgroups dispatched last are the shortest and fill the gaps left by
-    // earlier ones. Rows are ranked in LDS by every workgroup (R <= kLptRows;
-    // taller matrices have many more tiles than CUs and keep natural order).
-    // Snake: odd panels run ascending. Two workgroups that share a CU (or
-    // follow each other on it) then pair a long row with a short one.
-    int panel = tile / p.num_rows;
-    int target = tile % p.num_rows;
-    if (Cfg::kWGs > 1 && !(SPUTNIK_EXP & 256) && (panel & 1))
-      target = p.num_rows - 1 - target;
-#if defined(SPUTNIK_XJ) && SPUTNIK_XJ > 0
-    {
-      // Grouped XCD map (experiment): XCD x owns kXJ panels of one panel
-      // group and the rows of one rank class; slots s and s + T/16 (assumed
-      // to share a CU) pair local row q with its complement.
-      constexpr int kXJ = SPUTNIK_XJ;
-      const int R = p.num_rows, J = p.num_jtiles, NT = R * J;
-      const int njg = J / kXJ;
-      if (J % kXJ == 0 && njg > 0 && 8 % njg == 0 && NT % 16 == 0 &&
-          R % (2 * (8 / njg)) == 0 && gridDim.x == (unsigned)NT) {
-        const int nrs = 8 / njg;
-        const int x = blockIdx.x & 7;
-        const int s = blockIdx.x >> 3;
-        const int half = s / (NT / 16);
-        const int c = s % (NT / 16);
-        const int nr = R / nrs;
-        const int q = c / kXJ;
-        const int local = half == 0 ? q : nr - 1 - q;
-        target = local * nrs + x / njg;
-        panel = (x % njg) * kXJ + c % kXJ;
-      }
-    }
-#endif
-    j0 = panel * kBN;
-    srow = target;
-    if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
-      int *offs = reinterpret_cast<int *>(lds);
-      int *pick = offs + kLptRows + 1;
-      for (int r = tid; r <= p.num_rows; r += kThreads) offs[r] = p.s_offsets[r];
-      __syncthreads();
-      for (int r = tid; r < p.num_rows; r += kThreads) {
-        const int nr = offs[r + 1] - offs[r];
-        int rank = 0;
-        for (int r2 = 0; r2 < p.num_rows; ++r2) {
-          const int n2 = offs[r2 + 1] - offs[r2];
-          rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
-        }
-        if (rank == target) *pick = r;
-      }
-      __syncthreads();
-      srow = __builtin_amdgcn_readfirstlane(*pick);
-      entry0 = offs[srow];
-      entries = offs[srow + 1] - entry0;
-    } else {
-      entry0 = p.s_offsets[srow];
-      entries = p.s_offsets[srow + 1] - entry0;
-    }
-    nsteps = 0;
   }
 
   // ---- per-lane DMA offsets (relative to each step's tile base) ----------
@@ -386,34 +330,41 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       s_lk[q] = k;
     }
   }
+  // D offsets depend on the tile's dense origin j0 (range mask).
+  auto setup_d = [&](int j0) {
 #pragma unroll
-  for (int q = 0; q < kDInstr; ++q) {
-    const int g = wave * kDInstr + q;
-    bool ok;
-    if constexpr (kDKC) {
-      const int j = kKcRowsPerInstr * g + lane / kKcChunks;
-      const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(j);
-      d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
-      d_lk[q] = c * 8;
-      ok = j0 + j < p.j_limit;
-    } else {
-      const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
-      const int pc = lane % kDChunksPerRow;
-      const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
-      d_off[q] = (uint32_t)(k * p.d_ld + c * 16);
-      d_lk[q] = k;
-      ok = j0 + c * 8 < p.j_limit;
+    for (int q = 0; q < kDInstr; ++q) {
+      const int g = wave * kDInstr + q;
+      bool ok;
+      if constexpr (kDKC) {
+        const int j = kKcRowsPerInstr * g + lane / kKcChunks;
+        const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(j);
+        d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
+        d_lk[q] = c * 8;
+        ok = j0 + j < p.j_limit;
+      } else {
+        const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
+        const int pc = lane % kDChunksPerRow;
+        const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
+        d_off[q] = (uint32_t)(k * p.d_ld + c * 16);
+        d_lk[q] = k;
+        ok = j0 + c * 8 < p.j_limit;
+      }
+      if (!ok) d_off[q] = kOOB;
     }
-    if (!ok) d_off[q] = kOOB;
-  }
+  };
 
   f32x4 acc[kFM][kFN];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int a = 0; a < kFM; ++a)
+    for (int a = 0; a < kFM; ++a)
 #pragma unroll
-    for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
 
-  // Issue the DMA of pipeline step `step` into ring slot `slot`.
+  // Issue the DMA of pipeline step `step` into ring slot `slot`. Sparse S:
+  // `step` counts from the first entry staged in the LDS index list.
+  int srow = 0, j0 = 0;  // current tile
   auto issue = [&](int step, int slot) {
     if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
@@ -456,13 +407,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   };
 
   // Fragment registers of one k-step: [kk][f] for the S (a) and D (b)
-  // operands, kk = k-half 0..31 / 32..63.
+  // operands, kk = 32-deep MFMA k-step inside the slot.
   struct Frags {
     s16x8 a[kKK][kFM];
     s16x8 b[kKK][kFN];
   };
   auto read_step = [&](int slot, Frags &F) {
-    if constexpr ((SPUTNIK_EXP & 128) != 0) return;
     const char *simg = lds + slot * kStageBytes;
     const char *dimg = simg + kSBytes;
 #pragma unroll
@@ -515,23 +465,23 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
           acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
   };
 
-  // Software pipeline over k-steps. Ring slot of step s is s % 3. At the top
-  // of step s the fragments of s are already in registers (cur); the step
-  //   1. waits for its own DMA of step s+1 (counted vmcnt: s+2 stays in
+  // Software pipeline over k-steps [first, first + steps) (issue() indices).
+  // Ring slot of the i-th step is i % 3. At the top of step i the fragments
+  // of i are already in registers (cur); the step
+  //   1. waits for its own DMA of step i+1 (counted vmcnt: i+2 stays in
   //      flight) and meets the other waves at a raw s_barrier, after which
-  //      step s+1's slot is complete and step s's slot is no longer read;
-  //   2. refills step s's slot with the DMA of step s+3;
-  //   3. issues the LDS reads of step s+1 into `next` and, without waiting for
-  //      them, the 32 MFMAs of step s on `cur`;
+  //      step i+1's slot is complete and step i's slot is no longer read;
+  //   2. refills step i's slot with the DMA of step i+3;
+  //   3. issues the LDS reads of step i+1 into `next` and, without waiting for
+  //      them, the MFMAs of step i on `cur`;
   //   4. waits for `next`.
   // DMA therefore has two steps of MFMA time to land and the LDS read latency
-  // hides under the MFMAs.
-  unsigned long long acct[4] = {0, 0, 0, 0};
-  auto pipeline = [&](int steps) {
+  // hides under the MFMAs. The ring is fully drained on return.
+  auto pipeline = [&](int first, int steps) {
     if (steps <= 0) return;
-    issue(0, 0);
-    if (steps > 1) issue(1, 1);
-    if (steps > 2) issue(2, 2);
+    issue(first, 0);
+    if (steps > 1) issue(first + 1, 1);
+    if (steps > 2) issue(first + 2, 2);
     if (steps > 2)
       wait_vmcnt<2 * kGroup>();
     else if (steps > 1)
@@ -542,146 +492,376 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     Frags f0, f1;
     read_step(0, f0);
     wait_step(f0);
-    int slot = 0;  // slot of step s
-    auto body = [&](int s, Frags &cur, Frags &next) {
+    int slot = 0;  // slot of step i
+    auto body = [&](int i, Frags &cur, Frags &next) {
       const int nslot = slot + 1 == kStages ? 0 : slot + 1;
-      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-      if constexpr ((SPUTNIK_EXP & 32) != 0) t0 = __builtin_amdgcn_s_memtime();
-      if (s + 1 < steps) {
-        if (s + 2 < steps)
+      if (i + 1 < steps) {
+        if (i + 2 < steps)
           wait_vmcnt<kGroup>();
         else
           wait_vmcnt<0>();
-        if constexpr ((SPUTNIK_EXP & 32) != 0) t1 = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_barrier();
-        if constexpr ((SPUTNIK_EXP & 32) != 0) t2 = __builtin_amdgcn_s_memtime();
-        if (s + 3 < steps) issue(s + 3, slot);
+        if (i + 3 < steps) issue(first + i + 3, slot);
         read_step(nslot, next);
       }
       mfma_step(cur);
-      if constexpr ((SPUTNIK_EXP & 32) != 0) t3 = __builtin_amdgcn_s_memtime();
-      if (s + 1 < steps) wait_step(next);
-      if constexpr ((SPUTNIK_EXP & 32) != 0) {
-        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
-        if (s + 1 < steps) {
-          acct[0] += t1 - t0;
-          acct[1] += t2 - t1;
-          acct[2] += t3 - t2;
-          acct[3] += t4 - t3;
-        }
-      }
+      if (i + 1 < steps) wait_step(next);
       slot = nslot;
     };
-    for (int s = 0; s < steps; s += 2) {
-      body(s, f0, f1);
-      if (s + 1 < steps) body(s + 1, f1, f0);
+    for (int i = 0; i < steps; i += 2) {
+      body(i, f0, f1);
+      if (i + 1 < steps) body(i + 1, f1, f0);
     }
   };
 
-  exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
-  if constexpr (kSparseOut) {
-    exp_stamp(p.debug, 7, nsteps);
-    pipeline(nsteps);
-  } else {
-    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
+  // Steps [s_begin, s_end) of sparse block-row `srow` whose entries start at
+  // entry0 (entry e covers steps e*kStepsPerBlock ..). The (k-block, storage
+  // block) list is staged into LDS in chunks of kIndexChunk entries.
+  auto run_sparse = [&](int entry0, int s_begin, int s_end) {
     const bool col_order = p.s_block_offsets != nullptr;
-    for (int base = 0; base < entries; base += kIndexChunk) {
-      const int n = min(kIndexChunk, entries - base);
-      __syncthreads();  // previous chunk fully consumed (ring and index list)
+    const int e_begin = s_begin / kStepsPerBlock;
+    const int e_end = (s_end + kStepsPerBlock - 1) / kStepsPerBlock;
+    for (int cb = e_begin; cb < e_end; cb += kIndexChunk) {
+      const int n = min(kIndexChunk, e_end - cb);
+      __syncthreads();  // ring, staging and index list no longer read
       for (int e = tid; e < n; e += kThreads) {
-        const int ge = entry0 + base + e;
+        const int ge = entry0 + cb + e;
         idx_kc[e] = p.s_indices[ge];
         idx_blk[e] = col_order ? p.s_block_offsets[ge] : ge;
       }
       __syncthreads();
-      pipeline(kStepsPerBlock * n);
+      const int lo = max(s_begin, cb * kStepsPerBlock);
+      const int hi = min(s_end, (cb + n) * kStepsPerBlock);
+      pipeline(lo - cb * kStepsPerBlock, hi - lo);
     }
-  }
+  };
 
-  // ---- epilogue: fp32 -> T, staged through LDS, 16-byte coalesced stores --
-  wait_vmcnt<0>();
-  exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
-  __syncthreads();
-  // The tile is staged in kPasses slices of kPassJ dense columns (j) when
-  // the whole tile does not fit in the ring (128 x 512 tiles).
-  constexpr int kStLdNT = kBN * 2 + 16;  // straight staging row: j-contiguous
-  constexpr int kStLdT = kBM * 2 + 16;   // transposed staging row
-  constexpr int kPasses =
-      kOutT ? ((kBN * kStLdT + kRingBytes - 1) / kRingBytes)
-            : ((kBM * kStLdNT + kRingBytes - 1) / kRingBytes);
-  constexpr int kPassJ = kBN / kPasses;
-  static_assert(kPassJ % 16 == 0 && kPassJ * kPasses == kBN, "passes");
-  constexpr int kOutRows = kOutT ? kPassJ : kBM;  // staging rows per pass
-  constexpr int kOutCols = kOutT ? kBM : kPassJ;
-  constexpr int kStLd = kOutCols * 2 + 16;  // padded staging row (bytes)
-  static_assert(kOutRows * kStLd <= kRingBytes, "staging fits in the ring");
-  char *st = lds;
+  // ---- output of one finished tile: fp32 -> T, staged through LDS, 16-byte
+  // coalesced stores. The tile is staged in kPasses slices of kPassJ dense
+  // columns (j) when it does not fit in the ring at once (128 x 512 tiles).
+  auto write_tile = [&](long long out_block) {
+    wait_vmcnt<0>();
+    __syncthreads();
+    constexpr int kStLdNT = kBN * 2 + 16;  // straight staging row
+    constexpr int kStLdT = kBM * 2 + 16;   // transposed staging row
+    constexpr int kPasses =
+        kOutT ? ((kBN * kStLdT + kRingBytes - 1) / kRingBytes)
+              : ((kBM * kStLdNT + kRingBytes - 1) / kRingBytes);
+    constexpr int kPassJ = kBN / kPasses;
+    static_assert(kPassJ % 16 == 0 && kPassJ * kPasses == kBN, "passes");
+    constexpr int kOutRows = kOutT ? kPassJ : kBM;  // staging rows per pass
+    constexpr int kOutCols = kOutT ? kBM : kPassJ;
+    constexpr int kStLd = kOutCols * 2 + 16;  // padded staging row (bytes)
+    static_assert(kOutRows * kStLd <= kRingBytes, "staging fits in the ring");
+    char *st = lds;
 #pragma unroll
-  for (int pass = 0; pass < kPasses; ++pass) {
-    const int jp0 = pass * kPassJ;
-    if (pass > 0) __syncthreads();  // previous slice fully stored
+    for (int pass = 0; pass < kPasses; ++pass) {
+      const int jp0 = pass * kPassJ;
+      if (pass > 0) __syncthreads();  // previous slice fully stored
 #pragma unroll
-    for (int a = 0; a < kFM; ++a) {
+      for (int a = 0; a < kFM; ++a) {
 #pragma unroll
-      for (int b = 0; b < kFN; ++b) {
-        const int jb = col_w + 16 * b;  // wave-uniform
-        if (jb < jp0 || jb >= jp0 + kPassJ) continue;
-        const int i = row_w + 16 * a + 4 * (lane >> 4);
-        const int j = jb - jp0 + (lane & 15);
-        if constexpr (kOutT) {
-          typedef T t4 __attribute__((ext_vector_type(4)));
-          t4 v;
-          v[0] = (T)acc[a][b][0];
-          v[1] = (T)acc[a][b][1];
-          v[2] = (T)acc[a][b][2];
-          v[3] = (T)acc[a][b][3];
-          *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
-        } else {
+        for (int b = 0; b < kFN; ++b) {
+          const int jb = col_w + 16 * b;  // wave-uniform
+          if (jb < jp0 || jb >= jp0 + kPassJ) continue;
+          const int i = row_w + 16 * a + 4 * (lane >> 4);
+          const int j = jb - jp0 + (lane & 15);
+          if constexpr (kOutT) {
+            typedef T t4 __attribute__((ext_vector_type(4)));
+            t4 v;
+            v[0] = (T)acc[a][b][0];
+            v[1] = (T)acc[a][b][1];
+            v[2] = (T)acc[a][b][2];
+            v[3] = (T)acc[a][b][3];
+            *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
-                (T)acc[a][b][r];
+            for (int r = 0; r < 4; ++r)
+              *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
+                  (T)acc[a][b][r];
+          }
         }
       }
-    }
-    __syncthreads();
-    constexpr int kChunksPerRow = kOutCols / 8;
-    constexpr int kChunks = kOutRows * kChunksPerRow;
-    for (int id = tid; id < kChunks; id += kThreads) {
-      const int row = id / kChunksPerRow;
-      const int cc = id % kChunksPerRow;
-      const uint4 v =
-          *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
-      char *dst;
-      if constexpr (kSparseOut) {
-        dst = p.c_data + out_block * (kBlock * kBlock * 2) +
-              row * (kBlock * 2) + cc * 16;
-      } else if constexpr (kOutT) {
-        const int jrow = j0 + jp0 + row;
-        if (jrow >= p.j_limit) continue;
-        dst = p.c_data + (long long)jrow * p.c_ld +
-              ((long long)srow * kBM + cc * 8) * 2;
-      } else {
-        const int jcol = j0 + jp0 + cc * 8;
-        if (jcol >= p.j_limit) continue;
-        dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
-              (long long)jcol * 2;
+      __syncthreads();
+      constexpr int kChunksPerRow = kOutCols / 8;
+      constexpr int kChunks = kOutRows * kChunksPerRow;
+      for (int id = tid; id < kChunks; id += kThreads) {
+        const int row = id / kChunksPerRow;
+        const int cc = id % kChunksPerRow;
+        const uint4 v =
+            *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
+        char *dst;
+        if constexpr (kSparseOut) {
+          dst = p.c_data + out_block * (kBlock * kBlock * 2) +
+                row * (kBlock * 2) + cc * 16;
+        } else if constexpr (kOutT) {
+          const int jrow = j0 + jp0 + row;
+          if (jrow >= p.j_limit) continue;
+          dst = p.c_data + (long long)jrow * p.c_ld +
+                ((long long)srow * kBM + cc * 8) * 2;
+        } else {
+          const int jcol = j0 + jp0 + cc * 8;
+          if (jcol >= p.j_limit) continue;
+          dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
+                (long long)jcol * 2;
+        }
+        *reinterpret_cast<uint4 *>(dst) = v;
       }
-      *reinterpret_cast<uint4 *>(dst) = v;
+    }
+  };
+
+  if constexpr (!kStreamK) {
+    // ==== one output tile per workgroup ===================================
+    const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
+                                       : xcd_tile(blockIdx.x, gridDim.x);
+    long long out_block = 0;
+    int entry0 = 0, entries = 0;
+    if constexpr (kSparseOut) {
+      out_block = tile;
+      srow = p.c_row_indices[tile];
+      j0 = p.c_indices[tile] * kBlock;
+    } else {
+      // Longest-processing-time order: within each dense panel, tile t takes
+      // the block-row with the t-th most nonzeros (ties by row index), so the
+      // workgroups dispatched last are the shortest. Snake: odd panels run
+      // ascending, so two workgroups sharing a CU pair a long row with a
+      // short one. Rows are ranked in LDS (R <= kLptRows; taller matrices
+      // have many more tiles than CUs and keep natural order).
+      const int panel = tile / p.num_rows;
+      int target = tile % p.num_rows;
+      if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
+      j0 = panel * kBN;
+      srow = target;
+      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
+        int *offs = reinterpret_cast<int *>(lds);
+        for (int r = tid; r <= p.num_rows; r += kThreads)
+          offs[r] = p.s_offsets[r];
+        __syncthreads();
+        for (int r = tid; r < p.num_rows; r += kThreads) {
+          const int nr = offs[r + 1] - offs[r];
+          int rank = 0;
+          for (int r2 = 0; r2 < p.num_rows; ++r2) {
+            const int n2 = offs[r2 + 1] - offs[r2];
+            rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
+          }
+          if (rank == target) scratch[0] = r;
+        }
+        __syncthreads();
+        srow = __builtin_amdgcn_readfirstlane(scratch[0]);
+        entry0 = offs[srow];
+        entries = offs[srow + 1] - entry0;
+      } else {
+        entry0 = p.s_offsets[srow];
+        entries = p.s_offsets[srow + 1] - entry0;
+      }
+    }
+    setup_d(j0);
+    zero_acc();
+    exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
+    if constexpr (kSparseOut) {
+      const int nsteps = (p.k_limit + kBK - 1) / kBK;
+      exp_stamp(p.debug, 7, nsteps);
+      pipeline(0, nsteps);
+    } else {
+      exp_stamp(p.debug, 7, entries * kStepsPerBlock);
+      run_sparse(entry0, 0, entries * kStepsPerBlock);
+    }
+    exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
+    write_tile(out_block);
+  } else {
+    // ==== stream-K: persistent workgroups over an even split of k-steps ====
+    // Linear step order: panel-major, then CSR entry order: step g of the
+    // whole launch is (panel = g / P, entry = (g % P) / kStepsPerBlock, sub-
+    // step) with P = nnz_blocks * kStepsPerBlock. Tile (panel, row) covers
+    // [panel*P + offsets[row]*spb, panel*P + offsets[row+1]*spb).
+    const int R = p.num_rows;
+    const int G = p.sk_wgs;
+    const int w = xcd_tile(blockIdx.x, gridDim.x);  // XCD-contiguous ranges
+    const long long nnzb = p.s_offsets[R];
+    const long long P = nnzb * kStepsPerBlock;
+    const long long S = P * p.num_jtiles;
+    auto range_lo = [&](int v) { return S * v / G; };
+    const long long g0 = range_lo(w), g1 = range_lo(w + 1);
+
+    // Zero-fill the tiles of empty block-rows (no step covers them):
+    // workgroup w takes tiles w, w + G, ...
+    for (int t = w; t < R * p.num_jtiles; t += G) {
+      const int r = t % R;
+      if (p.s_offsets[r + 1] != p.s_offsets[r]) continue;
+      srow = r;
+      j0 = (t / R) * kBN;
+      zero_acc();
+      write_tile(0);
+    }
+
+    // Row containing CSR entry e: one parallel pass over offsets.
+    auto row_of = [&](long long e) {
+      __syncthreads();
+      for (int r = tid; r < R; r += kThreads)
+        if (p.s_offsets[r] <= e && e < p.s_offsets[r + 1]) scratch[1] = r;
+      __syncthreads();
+      return __builtin_amdgcn_readfirstlane(scratch[1]);
+    };
+    struct Seg {
+      int panel, row;
+      long long lo, hi;  // global steps covered by this workgroup
+      long long tb, te;  // the tile's global step range
+    };
+    auto tile_at = [&](long long g) {
+      Seg s;
+      s.panel = (int)(g / P);
+      s.row = row_of((g % P) / kStepsPerBlock);
+      s.tb = (long long)s.panel * P + (long long)p.s_offsets[s.row] * kStepsPerBlock;
+      s.te = (long long)s.panel * P +
+             (long long)p.s_offsets[s.row + 1] * kStepsPerBlock;
+      return s;
+    };
+    // Accumulate this workgroup's steps [lo, hi) of tile s into acc.
+    auto run_seg = [&](const Seg &s) {
+      srow = s.row;
+      j0 = s.panel * kBN;
+      setup_d(j0);
+      zero_acc();
+      run_sparse(p.s_offsets[s.row], (int)(s.lo - s.tb), (int)(s.hi - s.tb));
+    };
+    const long long kSlotFloats = (long long)kBM * kBN;
+    auto frag_ptr = [&](int slot, int a, int b) {
+      return reinterpret_cast<float4 *>(p.sk_partials + slot * kSlotFloats) +
+             ((wave * kFM + a) * kFN + b) * 64 + lane;
+    };
+    // Contributor: publish acc as this workgroup's partial (agent-scope
+    // release: stores, vmcnt(0) in every wave, barrier, release fence,
+    // vmcnt(0), relaxed flag store).
+    auto publish = [&]() {
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b) {
+          float4 v;
+          v.x = acc[a][b][0]; v.y = acc[a][b][1];
+          v.z = acc[a][b][2]; v.w = acc[a][b][3];
+          *frag_ptr(w, a, b) = v;
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.sk_flags + w, p.sk_epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    // Owner: add the partials of workgroups w-1, w-2, ... that cover the
+    // start of tile s (agent-scope acquire after one relaxed poll loop).
+    auto collect = [&](const Seg &s) {
+      for (int v = w - 1; v >= 0; --v) {
+        if (range_lo(v + 1) <= s.tb) break;  // v ends before the tile
+        if (range_lo(v) == range_lo(v + 1)) continue;  // empty range
+        if (tid == 0) {
+          int spins = 0;
+          while (__hip_atomic_load(p.sk_flags + v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) != p.sk_epoch &&
+                 spins < kSpinLimit) {
+            __builtin_amdgcn_s_sleep(2);
+            ++spins;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < kFM; ++a)
+#pragma unroll
+          for (int b = 0; b < kFN; ++b) {
+            const float4 v4 = *frag_ptr(v, a, b);
+            acc[a][b][0] += v4.x; acc[a][b][1] += v4.y;
+            acc[a][b][2] += v4.z; acc[a][b][3] += v4.w;
+          }
+        if (range_lo(v) <= s.tb) break;  // v holds the tile's first step
+      }
+    };
+
+    if (g0 < g1) {
+      Seg first = tile_at(g0);
+      first.lo = g0;
+      first.hi = min(g1, first.te);
+      const bool first_owner = first.lo > first.tb && first.hi == first.te;
+      Seg last = tile_at(g1 - 1);
+      last.lo = max(g0, last.tb);
+      last.hi = g1;
+      const bool single = last.tb == first.tb;
+      const bool contrib = single ? first.hi < first.te : last.hi < last.te;
+      exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
+      // Pieces in this order, through ONE pipeline call site (register
+      // pressure): (1) the contributed piece, so its owner never waits for
+      // it; (2) the whole tiles, whose steps form [whole_lo, whole_hi);
+      // (3) the owned tail of the first tile, whose contributors ran their
+      // pieces first.
+      const bool first_whole = first.lo == first.tb && first.hi == first.te;
+      const long long whole_lo = first_whole ? first.tb : first.te;
+      const long long whole_hi =
+          single ? (first_whole ? first.te : whole_lo)
+                 : (last.hi == last.te ? last.te : last.tb);
+      long long walk = whole_lo;
+      unsigned long long acct[4] = {0, 0, 0, 0};
+      bool contrib_done = !contrib, owner_done = !first_owner;
+      while (true) {
+        Seg piece;
+        int kind;  // 0 whole, 1 contributed, 2 owned
+        if (!contrib_done) {
+          piece = single ? first : last;
+          kind = 1;
+          contrib_done = true;
+        } else if (walk < whole_hi) {
+          piece = tile_at(walk);
+          piece.lo = piece.tb;
+          piece.hi = piece.te;
+          walk = piece.te;
+          kind = 0;
+        } else if (!owner_done) {
+          piece = first;
+          kind = 2;
+          owner_done = true;
+        } else {
+          break;
+        }
+        unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+        if constexpr ((SPUTNIK_EXP & 32) != 0) t0 = __builtin_amdgcn_s_memtime();
+        run_seg(piece);
+        if constexpr ((SPUTNIK_EXP & 32) != 0) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          t1 = __builtin_amdgcn_s_memtime();
+        }
+        if (kind == 1) {
+          publish();
+        } else {
+          if (kind == 2) collect(piece);
+          if constexpr ((SPUTNIK_EXP & 32) != 0) t2 = __builtin_amdgcn_s_memtime();
+          write_tile(0);
+        }
+        if constexpr ((SPUTNIK_EXP & 32) != 0) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          t3 = __builtin_amdgcn_s_memtime();
+          acct[0] += t1 - t0;
+          if (kind == 1) acct[1] += t3 - t1;
+          else { acct[2] += t2 - t1; acct[3] += t3 - t2; }
+        }
+      }
+      exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
+      if constexpr ((SPUTNIK_EXP & 32) != 0) {
+        exp_stamp(p.debug, 0, acct[0]);
+        exp_stamp(p.debug, 5, acct[1]);
+        exp_stamp(p.debug, 6, acct[2]);
+        exp_stamp(p.debug, 7, acct[3]);
+      }
     }
   }
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
-  if constexpr ((SPUTNIK_EXP & 32) != 0) {
-    // Overwrite the realtime / id slots with the wait accounting.
-    exp_stamp(p.debug, 0, acct[0]);
-    exp_stamp(p.debug, 5, acct[1]);
-    exp_stamp(p.debug, 6, acct[2] | (acct[3] << 32));
-  }
 }
 
 // Host-side launch of one instantiation (defined in block_gemm.hip).
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
-                           bool out_t, const GemmParams &params,
+                           bool out_t, bool stream_k, const GemmParams &params,
                            hipStream_t stream);
 
 }  // namespace sputnik_amd

@@ -18,6 +18,8 @@
 // A sparse S read in column order (DSD TN/TT, DDS NN/TN) uses the transposed
 // metadata (offsets_t, indices_t, block_offsets), exactly like the reference.
 #include <cstdint>
+#include <cstdlib>
+#include <mutex>
 
 #include "api_internal.h"
 #include "block_gemm.h"
@@ -29,6 +31,94 @@ namespace sputnik_amd {
 
 // Experiment builds (SPUTNIK_EXP & 16) copy this into GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
+
+// ---- stream-K workspace -------------------------------------------------
+// fp32 partial slots + hand-off flags for the persistent DSD/DDS grid, one
+// set per (device, stream) so concurrent streams never share slots. The
+// memory is allocated on the first eligible call and kept for the life of
+// the process (like a BLAS handle's workspace); it is never allocated while
+// the stream is being captured into a graph (that call runs one tile per
+// workgroup instead).
+struct StreamKSlot {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  float *partials = nullptr;
+  unsigned *flags = nullptr;
+  int wgs = 0;
+  unsigned epoch = 0;
+};
+constexpr int kMaxStreamKSlots = 16;
+static StreamKSlot g_sk[kMaxStreamKSlots];
+static std::mutex g_sk_mu;
+
+static bool StreamKEnabled() {
+#ifdef SPUTNIK_NO_STREAMK
+  return false;
+#endif
+  static const int enabled = [] {
+    // Off by default: correct, but the fp32 hand-off costs more than the
+    // balance it buys at the measured shapes.
+    const char *e = std::getenv("SPUTNIK_AMD_STREAMK");
+    return e ? std::atoi(e) : 0;
+  }();
+  return enabled != 0;
+}
+
+// Fills the stream-K fields of p; false = use one tile per workgroup.
+static bool PrepareStreamK(GemmParams *p, long long total_steps,
+                           hipStream_t stream) {
+  if (!StreamKEnabled() || total_steps <= 0) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  StreamKSlot *slot = nullptr;
+  for (auto &s : g_sk)
+    if (s.partials != nullptr && s.device == dev && s.stream == stream) {
+      slot = &s;
+      break;
+    }
+  if (slot == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+        cs != hipStreamCaptureStatusNone)
+      return false;
+    for (auto &s : g_sk)
+      if (s.partials == nullptr) {
+        slot = &s;
+        break;
+      }
+    if (slot == nullptr) return false;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                              dev) != hipSuccess || cus <= 0)
+      return false;
+    const int wgs = cus * CfgSparse::kWGs;
+    const size_t pbytes = (size_t)wgs * kBM * CfgSparse::kBN * sizeof(float);
+    float *partials = nullptr;
+    unsigned *flags = nullptr;
+    if (hipMalloc(&partials, pbytes) != hipSuccess) return false;
+    if (hipMalloc(&flags, wgs * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(flags, 0, wgs * sizeof(unsigned)) != hipSuccess) {
+      (void)hipFree(partials);
+      if (flags) (void)hipFree(flags);
+      return false;
+    }
+    slot->device = dev;
+    slot->stream = stream;
+    slot->partials = partials;
+    slot->flags = flags;
+    slot->wgs = wgs;
+  }
+  if (++slot->epoch == 0) slot->epoch = 1;
+  // At least ~16 k-steps per workgroup: tiny problems do not fan out into
+  // long hand-off chains.
+  const long long want = (total_steps + 15) / 16;
+  p->sk_wgs = (int)(want < slot->wgs ? want : slot->wgs);
+  p->sk_partials = slot->partials;
+  p->sk_flags = slot->flags;
+  p->sk_epoch = slot->epoch;
+  return true;
+}
 
 namespace {
 
@@ -217,7 +307,10 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
-  return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
+  const long long steps = (long long)(a.nonzeros / (kBlock * kBlock)) *
+                          (kBlock / CfgSparse::kBK) * p.num_jtiles;
+  const bool sk = PrepareStreamK(&p, steps, stream);
+  return LaunchBlockGemm(dtype, false, !ta, tb, false, sk, p, stream);
 }
 
 hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
@@ -232,8 +325,12 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
     const hipError_t e = BuildTransposed(b, stream);
     if (e != hipSuccess) return e;
   }
+  p.debug = g_debug;
+  const long long steps = (long long)(b.nonzeros / (kBlock * kBlock)) *
+                          (kBlock / CfgSparse::kBK) * p.num_jtiles;
+  const bool sk = PrepareStreamK(&p, steps, stream);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
-                         /*out_t=*/true, p, stream);
+                         /*out_t=*/true, sk, p, stream);
 }
 
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
@@ -243,8 +340,9 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   const Status st = PrepareSdd(a, ta, b, tb, c, &p);
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
-  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, p,
-                         stream);
+  p.debug = g_debug;
+  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, false,
+                         p, stream);
 }
 
 }  // namespace sputnik_amd
