@@ -41,7 +41,13 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=100,
+                    help="untimed calls first; >= ~10 ms of work so the clock "
+                         "has settled (the reference used 10 short calls)")
+    ap.add_argument("--workload", default="dsd",
+                    choices=["dsd", "sdd_dds", "moe", "panel"],
+                    help="dsd: the headline metric (BASELINE config 2); "
+                         "sdd_dds: config 3; moe: config 4; panel: config 5")
     ap.add_argument("--m", type=int, default=4096, help="rows per rank")
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--n", type=int, default=4096)
@@ -190,6 +196,161 @@ def cpu_baseline(prob: Problem, budget_s: float):
                    f"OpenMP over rows, fp32 in / double acc"),
     }
 
+class PairProblem:
+    """BASELINE config 3: MegaBlocks forward/backward pair at 4096^3, 20%:
+    SDD  C_bcsr = x . w (sparse output), then DDS  out = g . C_bcsr (C's
+    transposed metadata precomputed, as MegaBlocks caches it per topology).
+    FLOPs = 2 nnz K (SDD) + 2 nnz M (DDS)."""
+
+    def __init__(self, dim, density, dtype, seed, device):
+        import torch
+        import sputnik_amd as sp
+        from sputnik_amd import matrix_utils as mu
+        rng = np.random.default_rng(seed)
+        nz = mu.nonzeros_for_density(dim, dim, density)
+        nb = nz // (BLOCK * BLOCK)
+        off, idx = mu.random_topology(dim // BLOCK, dim // BLOCK, nb, rng)
+        td = torch.float16 if dtype == "f16" else torch.bfloat16
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed)
+        rnd = lambda n: (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
+        self.x, self.w, self.g = rnd(dim * dim), rnd(dim * dim), rnd(dim * dim)
+        self.out = torch.empty(dim * dim, dtype=td, device=device)
+        self.cv = torch.empty(nz, dtype=td, device=device)
+        self.C = sp.BlockMatrix(dim, dim, 128, nz, self.cv,
+                                torch.from_numpy(off).to(device),
+                                torch.from_numpy(idx.astype(np.int16)).to(device))
+        sp.AllocateRowIndicesBuffer(self.C)
+        sp.RowIndices(self.C, self.C.row_indices)
+        sp.AllocateTransposeBuffers(self.C)
+        sp.Transpose(self.C)
+        self.dim, self.nb = dim, nb
+        self.flops = 2.0 * nz * dim * 2
+        self.dtype_code = 0 if dtype == "f16" else 1
+        self.desc = (f"SDD(x,w)->C then DDS(g,C) block=128 M=K=N={dim} "
+                     f"density={density} {dtype} (MatmulEx metadata)")
+
+    def launcher(self):
+        import torch
+        import sputnik_amd as sp
+        L = sp.lib()
+        d = self.dim
+        cx, cw, cg, co = (sp.Matrix(d, d, t)._c() for t in (self.x, self.w, self.g, self.out))
+        cC = self.C._c()
+        stream = torch.cuda.current_stream().cuda_stream
+        a1 = (ctypes.byref(cx), 0, ctypes.byref(cw), 0, ctypes.byref(cC), self.dtype_code, stream)
+        a2 = (ctypes.byref(cg), 0, ctypes.byref(cC), 0, ctypes.byref(co), self.dtype_code, stream)
+        assert L.sputnik_sdd(*a1) == 0 and L.sputnik_dds_ex(*a2) == 0
+        self._keep = (cx, cw, cg, co, cC)
+        return lambda: (L.sputnik_sdd(*a1), L.sputnik_dds_ex(*a2))
+
+
+class MoeProblem:
+    """BASELINE config 4: MegaBlocks dMoE MLP, 8 experts, 8192 tokens,
+    d_model 4096, d_ff 14336, bf16. Block-diagonal-by-expert topology:
+    64 block-rows x 896 block-cols, 8 x 112 blocks per expert (12.5%).
+    One step = SDD h = x . w1 at the expert blocks + DSD y = h . w2."""
+
+    def __init__(self, dtype, seed, device, experts=8, tokens=8192,
+                 d_model=4096, d_ff=14336):
+        import torch
+        import sputnik_amd as sp
+        from sputnik_amd import matrix_utils as mu
+        rpe = tokens // experts // BLOCK
+        cpe = d_ff // BLOCK
+        off, idx = mu.expert_block_diagonal(experts, rpe, cpe)
+        nb = int(off[-1])
+        nz = nb * BLOCK * BLOCK
+        cols = experts * d_ff
+        td = torch.float16 if dtype == "f16" else torch.bfloat16
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed)
+        rnd = lambda n: (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
+        self.x = rnd(tokens * d_model)
+        self.w1 = rnd(d_model * cols)
+        self.w2 = rnd(cols * d_model)
+        self.y = torch.empty(tokens * d_model, dtype=td, device=device)
+        self.hv = torch.empty(nz, dtype=td, device=device)
+        self.H = sp.BlockMatrix(tokens, cols, 128, nz, self.hv,
+                                torch.from_numpy(off).to(device),
+                                torch.from_numpy(idx.astype(np.int16)).to(device))
+        sp.AllocateRowIndicesBuffer(self.H)
+        sp.RowIndices(self.H, self.H.row_indices)
+        self.dims = (tokens, d_model, cols)
+        self.flops = 2.0 * nz * d_model * 2
+        self.dtype_code = 0 if dtype == "f16" else 1
+        self.dtype_name = dtype
+        self.desc = (f"MoE {experts} experts tokens={tokens} d_model={d_model} "
+                     f"d_ff={d_ff} {dtype}: SDD(x,w1)->h + DSD(h,w2)")
+
+    def launcher(self):
+        import torch
+        import sputnik_amd as sp
+        L = sp.lib()
+        t, dm, cols = self.dims
+        cx = sp.Matrix(t, dm, self.x)._c()
+        c1 = sp.Matrix(dm, cols, self.w1)._c()
+        c2 = sp.Matrix(cols, dm, self.w2)._c()
+        cy = sp.Matrix(t, dm, self.y)._c()
+        cH = self.H._c()
+        stream = torch.cuda.current_stream().cuda_stream
+        a1 = (ctypes.byref(cx), 0, ctypes.byref(c1), 0, ctypes.byref(cH), self.dtype_code, stream)
+        a2 = (ctypes.byref(cH), 0, ctypes.byref(c2), 0, ctypes.byref(cy), self.dtype_code, stream)
+        assert L.sputnik_sdd(*a1) == 0 and L.sputnik_dsd_ex(*a2) == 0
+        self._keep = (cx, c1, c2, cy, cH)
+        return lambda: (L.sputnik_sdd(*a1), L.sputnik_dsd_ex(*a2))
+
+
+def run_other(args, world, rank, device):
+    """Non-headline BASELINE configs: one JSON line each (same contract)."""
+    import torch
+    if args.workload == "sdd_dds":
+        prob = PairProblem(args.k, 0.2, args.dtype, args.seed * 7919 + rank, device)
+        metric = "effective TFLOP/s (nnz-FLOPs) SDD+DDS pair block=128 M=K=N=4096 20%"
+    elif args.workload == "moe":
+        prob = MoeProblem("bf16", args.seed * 7919 + rank, device)
+        metric = "effective TFLOP/s (nnz-FLOPs) MoE SDD+DSD 8 experts bf16"
+    else:  # panel: config 5, M=131072 total, row panels over ranks
+        m_rank = 131072 // world
+        prob = Problem(m_rank, 4096, 4096, 0.02, args.dtype,
+                       args.seed * 7919 + rank, device)
+        prob.desc = (f"DSD block=128 M=131072 (/{world} ranks = {m_rank}) K=N=4096 "
+                     f"density=0.02 {args.dtype}")
+        metric = "effective TFLOP/s (nnz-FLOPs) row-panel DSD M=131072 K=N=4096 2%"
+    fn = prob.launcher()
+    ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
+    per = ms / args.steps
+    tflops = prob.flops * world / (per * 1e-3) / 1e12
+    extra = {}
+    if args.workload == "panel" and world > 1:
+        # Optional gather of the dense result (config 5): reported beside the
+        # hot path, never inside it.
+        import torch.distributed as dist
+        full = torch.empty(world * prob.c_vals.numel(), dtype=prob.c_vals.dtype,
+                           device=device)
+        dist.all_gather_into_tensor(full, prob.c_vals)
+        torch.cuda.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            dist.all_gather_into_tensor(full, prob.c_vals)
+        torch.cuda.synchronize()
+        ag = max_over_ranks((time.perf_counter() - t0) / 5 * 1e3, world)
+        extra["allgather_ms"] = round(ag, 4)
+        extra["allgather_GBps_per_rank"] = round(
+            full.numel() * full.element_size() * (world - 1) / world / (ag * 1e-3) / 1e9, 1)
+        del full
+    if rank == 0:
+        print(json.dumps({**extra,
+            "metric": metric, "value": round(tflops, 2), "unit": "TFLOP/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(per, 5), "higher_is_better": True,
+            "scaling": "weak" if args.workload != "panel" else "strong",
+            "vs_baseline": None,
+            "dtype": getattr(prob, "dtype_name", args.dtype),
+            "data": "synthetic", "config": {"workload": prob.desc},
+        }))
+
 
 def main():
     args = parse()
@@ -206,6 +367,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
+
+    if args.workload != "dsd":
+        run_other(args, world, rank, device)
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
 
     # Headline density first, then the sweep.
     densities = [args.density] + [float(d) for d in args.sweep.split(",")

@@ -77,13 +77,12 @@ def main():
         for k in ("start_skew_us", "wg_start_rt_us_pct", "distinct_cu", "steps", "cycles_per_step", "loop_fit"):
             res.pop(k, None)
     if args.acct:
-        vm = d[:, 0]; bar = d[:, 5]; iss = d[:, 6] & 0xFFFFFFFF; lg = d[:, 6] >> 32
+        parts = {"vmcnt_wait_barrier": d[:, 0], "dma_setup": d[:, 5] & 0xFFFFFFFF,
+                 "interleaved_issue": d[:, 5] >> 32, "unused": d[:, 6] & 0xFFFFFFFF,
+                 "read_wait": d[:, 6] >> 32}
         st = np.maximum(steps, 1)
-        res["per_step_cycles"] = {
-            "vmcnt_wait": round(float(np.sum(vm) / np.sum(st)), 1),
-            "barrier": round(float(np.sum(bar) / np.sum(st)), 1),
-            "issue_dma_reads_mfma": round(float(np.sum(iss) / np.sum(st)), 1),
-            "lgkm_wait": round(float(np.sum(lg) / np.sum(st)), 1)}
+        res["per_step_cycles"] = {k: round(float(np.sum(v) / np.sum(st)), 1)
+                                  for k, v in parts.items()}
         for k in ("start_skew_us", "wg_start_rt_us_pct", "distinct_cu"):
             res.pop(k, None)
     print(json.dumps(res))

@@ -32,47 +32,50 @@ namespace sputnik_amd {
 // Experiment builds (SPUTNIK_EXP & 16) copy this into GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
 
-// ---- stream-K workspace -------------------------------------------------
-// fp32 partial slots + hand-off flags for the persistent DSD/DDS grid, one
-// set per (device, stream) so concurrent streams never share slots. The
-// memory is allocated on the first eligible call and kept for the life of
-// the process (like a BLAS handle's workspace); it is never allocated while
-// the stream is being captured into a graph (that call runs one tile per
-// workgroup instead).
-struct StreamKSlot {
+// ---- pair-balancing workspace ---------------------------------------------
+// fp32 partial slots + hand-off flags, one set per (device, stream) so
+// concurrent streams never share them. Allocated on the first eligible call
+// and kept for the life of the process (like a BLAS handle's workspace);
+// never allocated while the stream is being captured into a graph (that call
+// runs one tile per workgroup instead). Flags return to 0 inside every
+// launch, so captured launches replay correctly.
+struct PairSlot {
   int device = -1;
   hipStream_t stream = nullptr;
   float *partials = nullptr;
   unsigned *flags = nullptr;
-  int wgs = 0;
-  unsigned epoch = 0;
+  int pairs = 0;  // capacity
+  int slots = 0;  // resident workgroups on the device
 };
-constexpr int kMaxStreamKSlots = 16;
-static StreamKSlot g_sk[kMaxStreamKSlots];
-static std::mutex g_sk_mu;
+constexpr int kMaxPairSlots = 16;
+static PairSlot g_pairs[kMaxPairSlots];
+static std::mutex g_pairs_mu;
 
-static bool StreamKEnabled() {
-#ifdef SPUTNIK_NO_STREAMK
+static bool PairsEnabled() {
+#ifdef SPUTNIK_NO_PAIRS
   return false;
 #endif
   static const int enabled = [] {
-    // Off by default: correct, but the fp32 hand-off costs more than the
-    // balance it buys at the measured shapes.
-    const char *e = std::getenv("SPUTNIK_AMD_STREAMK");
-    return e ? std::atoi(e) : 0;
+    const char *e = std::getenv("SPUTNIK_AMD_PAIRS");
+    return e ? std::atoi(e) : 1;
   }();
   return enabled != 0;
 }
 
-// Fills the stream-K fields of p; false = use one tile per workgroup.
-static bool PrepareStreamK(GemmParams *p, long long total_steps,
-                           hipStream_t stream) {
-  if (!StreamKEnabled() || total_steps <= 0) return false;
+// Fills the pair fields of p when pair balancing applies: every tile
+// resident at once (the point is the tail of a single wave of tiles), rows
+// rankable in-kernel, and a light row plus a heavy head fit the LDS index
+// list (k_blocks <= kIndexChunk).
+static void PreparePairs(GemmParams *p, int k_blocks, hipStream_t stream) {
+  p->pair = 0;
+  if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows ||
+      k_blocks > kIndexChunk)
+    return;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  std::lock_guard<std::mutex> lock(g_sk_mu);
-  StreamKSlot *slot = nullptr;
-  for (auto &s : g_sk)
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  PairSlot *slot = nullptr;
+  for (auto &s : g_pairs)
     if (s.partials != nullptr && s.device == dev && s.stream == stream) {
       slot = &s;
       break;
@@ -81,43 +84,41 @@ static bool PrepareStreamK(GemmParams *p, long long total_steps,
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
         cs != hipStreamCaptureStatusNone)
-      return false;
-    for (auto &s : g_sk)
+      return;
+    for (auto &s : g_pairs)
       if (s.partials == nullptr) {
         slot = &s;
         break;
       }
-    if (slot == nullptr) return false;
+    if (slot == nullptr) return;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
                               dev) != hipSuccess || cus <= 0)
-      return false;
-    const int wgs = cus * CfgSparse::kWGs;
-    const size_t pbytes = (size_t)wgs * kBM * CfgSparse::kBN * sizeof(float);
+      return;
+    const int slots = cus * CfgSparse::kWGs;
+    const int pairs = slots / 2;
     float *partials = nullptr;
     unsigned *flags = nullptr;
-    if (hipMalloc(&partials, pbytes) != hipSuccess) return false;
-    if (hipMalloc(&flags, wgs * sizeof(unsigned)) != hipSuccess ||
-        hipMemset(flags, 0, wgs * sizeof(unsigned)) != hipSuccess) {
+    if (hipMalloc(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
+                                 sizeof(float)) != hipSuccess)
+      return;
+    if (hipMalloc(&flags, pairs * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(flags, 0, pairs * sizeof(unsigned)) != hipSuccess) {
       (void)hipFree(partials);
       if (flags) (void)hipFree(flags);
-      return false;
+      return;
     }
     slot->device = dev;
     slot->stream = stream;
     slot->partials = partials;
     slot->flags = flags;
-    slot->wgs = wgs;
+    slot->pairs = pairs;
+    slot->slots = slots;
   }
-  if (++slot->epoch == 0) slot->epoch = 1;
-  // At least ~16 k-steps per workgroup: tiny problems do not fan out into
-  // long hand-off chains.
-  const long long want = (total_steps + 15) / 16;
-  p->sk_wgs = (int)(want < slot->wgs ? want : slot->wgs);
-  p->sk_partials = slot->partials;
-  p->sk_flags = slot->flags;
-  p->sk_epoch = slot->epoch;
-  return true;
+  if (p->num_tiles > slot->slots) return;
+  p->pair = 1;
+  p->pair_partials = slot->partials;
+  p->pair_flags = slot->flags;
 }
 
 namespace {
@@ -307,10 +308,8 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
-  const long long steps = (long long)(a.nonzeros / (kBlock * kBlock)) *
-                          (kBlock / CfgSparse::kBK) * p.num_jtiles;
-  const bool sk = PrepareStreamK(&p, steps, stream);
-  return LaunchBlockGemm(dtype, false, !ta, tb, false, sk, p, stream);
+  PreparePairs(&p, (ta ? a.rows : a.cols) / kBlock, stream);
+  return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
 }
 
 hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
@@ -326,11 +325,9 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
-  const long long steps = (long long)(b.nonzeros / (kBlock * kBlock)) *
-                          (kBlock / CfgSparse::kBK) * p.num_jtiles;
-  const bool sk = PrepareStreamK(&p, steps, stream);
+  PreparePairs(&p, (tb ? b.cols : b.rows) / kBlock, stream);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
-                         /*out_t=*/true, sk, p, stream);
+                         /*out_t=*/true, p, stream);
 }
 
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
@@ -341,8 +338,8 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
   p.debug = g_debug;
-  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, false,
-                         p, stream);
+  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, p,
+                         stream);
 }
 
 }  // namespace sputnik_amd

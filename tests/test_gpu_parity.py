@@ -144,6 +144,97 @@ def test_dsd_deterministic():
     assert torch.equal(outs[0], outs[1])
 
 
+def _skewed_topology(rows_b, cols_b, rng):
+    """Block-rows with very different lengths (0 .. cols_b blocks), so pair
+    balancing hands large heads from heavy to light rows."""
+    mask = np.zeros((rows_b, cols_b), dtype=bool)
+    for r in range(rows_b):
+        n = int(rng.integers(0, cols_b + 1))
+        mask[r, rng.choice(cols_b, n, replace=False)] = True
+    mask[0, :] = True          # one full row
+    mask[rows_b - 1, :] = False  # one empty row
+    return mu.mask_to_bcsr(mask)
+
+
+@pytest.mark.parametrize("op", ["dsd", "dds"])
+@pytest.mark.parametrize("rows_b", [2, 7, 32])
+def test_pair_balancing_skewed_rows(op, rows_b):
+    """Skewed row lengths through the pair-balanced schedule (every tile
+    resident): DSD NN and DDS NT (row-order S) and their column-order
+    variants, odd row counts (unpaired middle row), empty rows."""
+    rng = np.random.default_rng(rows_b)
+    kb = 24
+    for t in (False, True):
+        if op == "dsd":
+            # C[M x N] = op(A) B; S = op(A), whose block-rows are A's rows
+            # (NN) or, read through the transposed metadata, A's columns (TN).
+            top = _skewed_topology(kb, rows_b, rng) if t else \
+                _skewed_topology(rows_b, kb, rng)
+            nz = int(top[0][-1]) * 16384
+            A = H.HostSparse(*((kb * 128, rows_b * 128) if t else
+                               (rows_b * 128, kb * 128)), nz, rng,
+                             topology=top)
+            B = H.HostDense(kb * 128, 512, rng)
+            C, c_t = H.empty_dense(rows_b * 128, 512)
+            if t:
+                sp.AllocateTransposeBuffers(A.matrix)
+            sp.Matmul(A.matrix, t, B.matrix, False, C)
+            _sync()
+            amask = A.mask().T if t else A.mask()
+            ref = O.gemm(A.dense(), t, B.values, False, a_mask=amask,
+                         threads=H.oracle_threads())
+        else:
+            # C[M x N] = A op(B); S = op(B)^T: B's columns (NN, transposed
+            # metadata) or B's rows (NT).
+            top = _skewed_topology(rows_b, kb, rng) if t else \
+                _skewed_topology(kb, rows_b, rng)
+            nz = int(top[0][-1]) * 16384
+            Bs = H.HostSparse(*((rows_b * 128, kb * 128) if t else
+                                (kb * 128, rows_b * 128)), nz, rng,
+                              topology=top)
+            A = H.HostDense(384, kb * 128, rng)
+            C, c_t = H.empty_dense(384, rows_b * 128)
+            if not t:
+                sp.AllocateTransposeBuffers(Bs.matrix)
+            sp.Matmul(A.matrix, False, Bs.matrix, t, C)
+            _sync()
+            bmask = Bs.mask().T if t else Bs.mask()
+            ref = O.gemm(A.values, False, Bs.dense(), t, b_mask=bmask,
+                         threads=H.oracle_threads())
+        H.assert_close(c_t.float().cpu().numpy(), ref, "f16", f"{op} t={t}")
+
+
+def test_pair_balancing_graph_replay():
+    """The hand-off flags are reset inside each launch, so a captured launch
+    replays correctly (and repeated launches agree bit for bit)."""
+    rng = np.random.default_rng(9)
+    off, idx = _skewed_topology(16, 16, rng)
+    A = H.HostSparse(2048, 2048, int(off[-1]) * 16384, rng,
+                     topology=(off, idx))
+    B = H.HostDense(2048, 1024, rng)
+    C, c_t = H.empty_dense(2048, 1024)
+    sp.Matmul(A.matrix, False, B.matrix, False, C)  # workspace allocated
+    _sync()
+    first = c_t.clone()
+    ref = O.gemm(A.dense(), False, B.values, False, a_mask=A.mask(),
+                 threads=H.oracle_threads())
+    H.assert_close(first.float().cpu().numpy(), ref, "f16", "eager")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        sp.Matmul(A.matrix, False, B.matrix, False, C)  # this stream's slot
+    torch.cuda.current_stream().wait_stream(s)
+    _sync()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.Matmul(A.matrix, False, B.matrix, False, C)
+    for _ in range(5):
+        c_t.fill_(float("nan"))
+        g.replay()
+        _sync()
+        assert torch.equal(c_t, first)
+
+
 @pytest.mark.parametrize("density", [0.1, 0.3, 0.5, 0.9])
 def test_dsd_baseline_config_sampled(density):
     """BASELINE config 2 (M=K=N=4096) at its four densities: full GPU result,
@@ -296,6 +387,93 @@ def test_sdd_dds_pair_config3():
         H.assert_close(out_t[r * 128:(r + 1) * 128].float().cpu().numpy(),
                        ref, "f16", f"dds row-block {r}")
 
+
+
+def test_moe_config4_bf16_sampled():
+    """BASELINE config 4 at full size (8 experts, 8192 tokens, d_model 4096,
+    d_ff 14336, bf16, expert block-diagonal topology): SDD h = x.w1 at the
+    expert blocks, then DSD y = h.w2. Sampled blocks / row-blocks against the
+    oracle; host operands are drawn on the device and only the slices the
+    oracle needs come back."""
+    E, T, DM, FF = 8, 8192, 4096, 14336
+    cols = E * FF
+    rpe, cpe = T // E // 128, FF // 128
+    off, idx = mu.expert_block_diagonal(E, rpe, cpe)
+    nb = int(off[-1])
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    rnd = lambda *s: (torch.rand(*s, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
+    x, w1, w2 = rnd(T, DM), rnd(DM, cols), rnd(cols, DM)
+    hv = torch.full((nb, 128, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
+    Hm = sp.BlockMatrix(T, cols, 128, nb * 16384, hv,
+                        torch.from_numpy(off).cuda(),
+                        torch.from_numpy(idx.astype(np.int16)).cuda())
+    sp.AllocateRowIndicesBuffer(Hm)
+    sp.RowIndices(Hm, Hm.row_indices)
+    y = torch.full((T, DM), float("nan"), dtype=torch.bfloat16, device="cuda")
+    sp.Matmul(sp.Matrix(T, DM, x), False, sp.Matrix(DM, cols, w1), False, Hm)
+    sp.Matmul(Hm, False, sp.Matrix(cols, DM, w2), False, sp.Matrix(T, DM, y))
+    _sync()
+    f = lambda t: t.float().cpu().numpy()
+    rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    for b in (0, 1000, nb // 2 + 37, nb - 1):
+        r, c = int(rows[b]), int(idx[b])
+        ref = O.gemm(f(x[r * 128:(r + 1) * 128]), False,
+                     f(w1[:, c * 128:(c + 1) * 128]), False,
+                     threads=H.oracle_threads())
+        H.assert_close(f(hv[b]), ref, "bf16", f"moe sdd block {b}")
+    for r in (0, 29, 63):
+        e = r // rpe
+        h_row = f(hv[off[r]:off[r + 1]]).transpose(1, 0, 2).reshape(128, FF)
+        ref = O.gemm(h_row, False, f(w2[e * FF:(e + 1) * FF]), False,
+                     threads=H.oracle_threads())
+        H.assert_close(f(y[r * 128:(r + 1) * 128]), ref, "bf16",
+                       f"moe dsd row-block {r}")
+
+
+def test_tall_panel_config5_sampled():
+    """BASELINE config 5 at full size on one device: DSD M=131072, K=N=4096,
+    2% density (656 blocks over 1024 block-rows, most rows empty). Empty
+    block-rows must be exact zeros; sampled non-empty rows against the
+    oracle; and the per-rank row-panel split (shard_rows_by_nnz) run as
+    separate calls reproduces the single-call result bit-exactly."""
+    rng = np.random.default_rng(5)
+    M = 131072
+    nz = mu.nonzeros_for_density(M, 4096, 0.02)
+    A = H.HostSparse(M, 4096, nz, rng)
+    B = H.HostDense(4096, 4096, rng)
+    C, c_t = H.empty_dense(M, 4096)
+    sp.Matmul(A.matrix, False, B.matrix, False, C)
+    _sync()
+    counts = np.diff(A.offsets)
+    empty = np.nonzero(counts == 0)[0]
+    assert len(empty) > 0
+    e_rows = torch.from_numpy(empty).cuda()
+    blk = c_t.view(M // 128, 128, 4096)
+    assert int(torch.count_nonzero(blk[e_rows])) == 0
+    nonempty = np.nonzero(counts)[0]
+    for r in (nonempty[0], nonempty[len(nonempty) // 2], nonempty[-1]):
+        o0, o1 = A.offsets[r], A.offsets[r + 1]
+        a_row = mu.to_dense(128, 4096, np.array([0, o1 - o0], np.int32),
+                            A.indices[o0:o1], A.values[o0:o1])
+        ref = O.gemm(a_row, False, B.values, False, threads=H.oracle_threads())
+        H.assert_close(c_t[r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
+                       "f16", f"panel row-block {r}")
+    # Row panels as 8 ranks would run them: same bits.
+    for r0, r1 in mu.shard_rows_by_nnz(A.offsets, 8):
+        if r1 == r0:
+            continue
+        po, pi, pv = mu.slice_block_rows(A.offsets, A.indices, A.values, r0, r1)
+        nbp = len(pi)
+        Pm = sp.BlockMatrix((r1 - r0) * 128, 4096, 128, nbp * 16384,
+                            A.dev_values[A.offsets[r0]:A.offsets[r1]]
+                            if nbp else A.dev_values,
+                            torch.from_numpy(po).cuda(),
+                            torch.from_numpy(pi.astype(np.int16)).cuda())
+        Cp, cp_t = H.empty_dense((r1 - r0) * 128, 4096)
+        sp.Matmul(Pm, False, B.matrix, False, Cp)
+        _sync()
+        assert torch.equal(cp_t, c_t[r0 * 128:r1 * 128])
 
 # ------------------------------------------------------------ metadata ----
 
