@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--density", type=float, default=0.5)
     ap.add_argument("--m", type=int, default=4096)
     ap.add_argument("--acct", action="store_true")
-    ap.add_argument("--skacct", action="store_true")
+    ap.add_argument("--dump", default="", help="save the raw per-workgroup stamps (.npy)")
     args = ap.parse_args()
     import torch
     import bench
@@ -41,11 +41,14 @@ def main():
     torch.cuda.synchronize()
     d = dbg.cpu().numpy().reshape(tiles, 8).astype(np.int64)
     d = d[d[:, 4] != 0]
+    if args.dump:
+        np.save(args.dump, d)
     tiles = len(d)
     rt0 = d[:, 0] - d[:, 0].min()
     pro = d[:, 2] - d[:, 1]
-    loop = d[:, 3] - d[:, 2]
-    epi = d[:, 4] - d[:, 3]
+    wall_us = (d[:, 3] - d[:, 0]) / 100.0           # realtime: 100 MHz
+    loop = d[:, 4] - d[:, 2]                         # loop + epilogue cycles
+    epi = np.zeros_like(loop)
     tot = d[:, 4] - d[:, 1]
     steps = d[:, 7]
     cu = (d[:, 5] << 16) | (d[:, 6] & 0xFFFF)
@@ -61,21 +64,15 @@ def main():
         "cycles_per_step": round(float(np.sum(loop) / max(1, np.sum(steps))), 1),
         "steps": [int(steps.min()), int(np.median(steps)), int(steps.max())],
         "distinct_cu": int(len(np.unique(cu))),
+        "wall_us_pct": [round(float(np.percentile(wall_us, q)), 2) for q in (0, 50, 90, 100)],
+        "end_rt_us_pct": [round(float(np.percentile((d[:, 3] - d[:, 0].min()) / 100.0, q)), 2) for q in (0, 50, 90, 100)],
+        "clock_ghz_pct": [round(float(np.percentile((d[:, 4] - d[:, 1]) / np.maximum(d[:, 3] - d[:, 0], 1) / 10.0, q)), 3) for q in (0, 50, 100)],
         "wg_start_rt_us_pct": [round(float(np.percentile(rt0, q)) / 100.0, 2) for q in (0, 25, 50, 75, 90, 100)],
     }
     # Correlation of loop time with steps (slope = cycles/step, intercept).
     A = np.vstack([steps, np.ones_like(steps)]).T.astype(float)
     slope, icpt = np.linalg.lstsq(A, loop.astype(float), rcond=None)[0]
     res["loop_fit"] = {"cycles_per_step": round(slope, 1), "intercept": round(icpt, 1)}
-    if args.skacct:
-        res["sk_cycles_median"] = {
-            "pipeline": int(np.median(d[:, 0])), "publish": int(np.median(d[:, 5])),
-            "collect": int(np.median(d[:, 6])), "write": int(np.median(d[:, 7]))}
-        res["sk_cycles_max"] = {
-            "pipeline": int(d[:, 0].max()), "publish": int(d[:, 5].max()),
-            "collect": int(d[:, 6].max()), "write": int(d[:, 7].max())}
-        for k in ("start_skew_us", "wg_start_rt_us_pct", "distinct_cu", "steps", "cycles_per_step", "loop_fit"):
-            res.pop(k, None)
     if args.acct:
         parts = {"vmcnt_wait_barrier": d[:, 0], "dma_setup": d[:, 5] & 0xFFFFFFFF,
                  "interleaved_issue": d[:, 5] >> 32, "unused": d[:, 6] & 0xFFFFFFFF,

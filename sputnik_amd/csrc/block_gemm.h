@@ -46,7 +46,6 @@
 //   1: skip the MFMAs (keep LDS reads)   2: skip the operand DMA
 //   4: no LPT row order                  8: no XCD-aware tile map
 //  16: per-workgroup s_memtime phase stamps into GemmParams::debug
-// 128: (with 16) wave 0's cycles per pipeline phase into debug slots 0, 5, 6
 //  64: every DMA re-reads the first step's tiles (cache-resident: isolates
 //      the memory system from the LDS-write / issue cost of the DMA)
 #ifndef SPUTNIK_EXP
@@ -89,14 +88,6 @@ struct GemmParams {
   int j_limit;                 // dense extent (elements) of the j dimension
   int k_limit;                 // SDD: K (elements)
   int num_tiles;               // output tiles (one-tile-per-workgroup grid)
-  // Pair balancing (sparse-row products, see the kernel): the block-rows of
-  // each panel are paired heaviest-with-lightest; the light workgroup also
-  // computes the head of the heavy row and hands it over as an fp32
-  // partial. pair == 0: one tile per workgroup in LPT order.
-  int pair;
-  float *pair_partials;        // (#pairs) x (128 x BN) fp32
-  unsigned *pair_flags;        // #pairs; 1 = partial published, reset by
-                               // the consumer (graph-replay safe)
   unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
 };
 
@@ -137,8 +128,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char *base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0,
@@ -194,7 +183,7 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
 
 // Experiment builds: record (wave 0, lane 0) a per-workgroup timeline.
 // Layout per workgroup: [realtime start, memtime start, memtime prologue end,
-// memtime loop end, memtime end, xcc_id, hw_id, k-steps].
+// realtime loop end, memtime end, xcc_id, hw_id, k-steps].
 __device__ __forceinline__ void exp_stamp(unsigned long long *dbg, int slot,
                                           unsigned long long v) {
   if constexpr ((SPUTNIK_EXP & 16) != 0) {
@@ -234,8 +223,8 @@ using CfgQuad = TileConfig<256, 1, 2, 32, 3, 2>;
 // 128x512 tile, 4 waves of 128x128, BK=32, one workgroup per CU (measured
 // slower than CfgDual: DESIGN.md §10).
 using CfgWide512 = TileConfig<512, 1, 4, 32, 3, 1>;
-// 128x512 tile, 8 waves of 64x128, BK=32, one workgroup per CU: 17% fewer
-// DMA bytes per FLOP than two CfgDual workgroups.
+// 128x512 tile, 8 waves of 64x128, BK=32, one workgroup per CU (measured
+// slower than CfgDual without cross-workgroup balancing: DESIGN.md §10).
 using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
@@ -244,12 +233,6 @@ using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 #define SPUTNIK_SPARSE_CFG CfgDual
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
-
-// Bounded spin for the pair hand-off (about 0.1 s): a launch can never hang
-// on a missing partial. The producer never waits and always has a lower
-// workgroup index than its consumer (in-order dispatch), so the bound is a
-// guard, not part of the protocol.
-constexpr int kSpinLimit = 1 << 22;
 
 // kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
@@ -359,7 +342,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
   };
 
-  unsigned long long acct[5] = {0, 0, 0, 0, 0};  // SPUTNIK_EXP & 128
   f32x4 acc[kFM][kFN];
   auto zero_acc = [&]() {
 #pragma unroll
@@ -368,104 +350,76 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  // ---- one pipeline step, split into units that the body interleaves ----
-  // DMA: prep_issue() computes the step's buffer descriptors (SALU only);
-  // issue_one(c, q) issues DMA instruction q of this wave (kNDma per step).
-  // Sparse S: (kblk, blk) = (k-block, storage block) of the step's entry,
-  // read from the LDS index list one step ahead (see pipeline).
-  constexpr int kNDma = kSInstr + kDInstr;
+  // Issue the DMA of pipeline step `step` into ring slot `slot`. Sparse S:
+  // `step` counts from the first entry staged in the LDS index list.
   int srow = 0, j0 = 0;  // current tile
-  struct IssueCtx {
-    __amdgpu_buffer_rsrc_t rs, rd;
-    char *slot_base;
-    int krem;  // valid k in this step (SDD tail)
-  };
-  auto prep_issue = [&](int step, int slot, int kblk, int blk) {
+  auto issue = [&](int step, int slot) {
+    if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
     const char *s_base;
     const char *d_base;
-    IssueCtx c;
-    c.krem = kBK;
+    int krem = kBK;  // valid k in this step (SDD tail)
     if constexpr (kSparseOut) {
       const long long k0 = (long long)step * kBK;
-      c.krem = p.k_limit - (int)k0;
+      krem = p.k_limit - (int)k0;
       s_base = kSKC ? p.s_data + (long long)srow * kBM * p.s_ld + k0 * 2
                     : p.s_data + k0 * p.s_ld + (long long)srow * kBM * 2;
       d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + k0 * 2
                     : p.d_data + k0 * p.d_ld + (long long)j0 * 2;
     } else {
+      const int e = step / kStepsPerBlock;
       const int h = step % kStepsPerBlock;
+      const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
+      const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
       s_base = p.s_data + (long long)blk * (kBlock * kBlock * 2) +
                (kSKC ? h * (kBK * 2) : h * (kBK * 256));
       const long long kg = (long long)kblk * kBlock + h * kBK;
       d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
                     : p.d_data + kg * p.d_ld + (long long)j0 * 2;
     }
-    c.slot_base = lds + slot * kStageBytes;
-    c.rs = make_rsrc(s_base);
-    c.rd = make_rsrc(d_base);
-    return c;
-  };
-  auto issue_one = [&](const IssueCtx &c, int q) {
-    if constexpr ((SPUTNIK_EXP & 2) != 0) return;
-    if (q < kSInstr) {
-      uint32_t off = s_off[q];
-      if constexpr (kSparseOut) off = s_lk[q] < c.krem ? off : kOOB;
-      dma16(c.rs, c.slot_base + (wave * kSInstr + q) * 1024, off);
-    } else {
-      const int qd = q - kSInstr;
-      uint32_t off = d_off[qd];
-      if constexpr (kSparseOut) off = d_lk[qd] < c.krem ? off : kOOB;
-      dma16(c.rd, c.slot_base + kSBytes + (wave * kDInstr + qd) * 1024, off);
-    }
-  };
-  // The (k-block, storage block) of pipeline step `step` (sparse S).
-  auto step_index = [&](int step, int &kblk, int &blk) {
-    if constexpr (!kSparseOut) {
-      const int e = step / kStepsPerBlock;
-      kblk = idx_kc[e];
-      blk = idx_blk[e];
-    }
-  };
-  auto issue = [&](int step, int slot) {
-    int kblk = 0, blk = 0;
-    step_index(step, kblk, blk);
-    const IssueCtx c = prep_issue(step, slot,
-                                  __builtin_amdgcn_readfirstlane(kblk),
-                                  __builtin_amdgcn_readfirstlane(blk));
+    char *slot_base = lds + slot * kStageBytes;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(s_base);
+    const __amdgpu_buffer_rsrc_t rd = make_rsrc(d_base);
 #pragma unroll
-    for (int q = 0; q < kNDma; ++q) issue_one(c, q);
+    for (int q = 0; q < kSInstr; ++q) {
+      uint32_t off = s_off[q];
+      if constexpr (kSparseOut) off = s_lk[q] < krem ? off : kOOB;
+      dma16(rs, slot_base + (wave * kSInstr + q) * 1024, off);
+    }
+#pragma unroll
+    for (int q = 0; q < kDInstr; ++q) {
+      uint32_t off = d_off[q];
+      if constexpr (kSparseOut) off = d_lk[q] < krem ? off : kOOB;
+      dma16(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024, off);
+    }
   };
 
   // Fragment registers of one k-step: [kk][f] for the S (a) and D (b)
-  // operands, kk = 32-deep MFMA k-step inside the slot. Read unit u is
-  // fragment u of the order (kk, S frags, D frags).
+  // operands, kk = 32-deep MFMA k-step inside the slot.
   struct Frags {
     s16x8 a[kKK][kFM];
     s16x8 b[kKK][kFN];
   };
-  constexpr int kNRead = kKK * (kFM + kFN);
-  auto read_one = [&](int slot, Frags &F, int u) {
+  auto read_step = [&](int slot, Frags &F) {
     const char *simg = lds + slot * kStageBytes;
     const char *dimg = simg + kSBytes;
-    const int kk = u / (kFM + kFN);
-    const int f = u % (kFM + kFN);
-    if (f < kFM) {
-      if constexpr (kSKC)
-        F.a[kk][f] = read_kc<kKcRow>(simg, row_w + 16 * f, kk, lane);
-      else
-        F.a[kk][f] = read_mn<kBM * 2>(simg, row_w + 16 * f, kk, lane);
-    } else {
-      const int fb = f - kFM;
-      if constexpr (kDKC)
-        F.b[kk][fb] = read_kc<kKcRow>(dimg, col_w + 16 * fb, kk, lane);
-      else
-        F.b[kk][fb] = read_mn<kDRowBytes>(dimg, col_w + 16 * fb, kk, lane);
-    }
-  };
-  auto read_step = [&](int slot, Frags &F) {
 #pragma unroll
-    for (int u = 0; u < kNRead; ++u) read_one(slot, F, u);
+    for (int kk = 0; kk < kKK; ++kk) {
+#pragma unroll
+      for (int f = 0; f < kFM; ++f) {
+        if constexpr (kSKC)
+          F.a[kk][f] = read_kc<kKcRow>(simg, row_w + 16 * f, kk, lane);
+        else
+          F.a[kk][f] = read_mn<kBM * 2>(simg, row_w + 16 * f, kk, lane);
+      }
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) {
+        if constexpr (kDKC)
+          F.b[kk][f] = read_kc<kKcRow>(dimg, col_w + 16 * f, kk, lane);
+        else
+          F.b[kk][f] = read_mn<kDRowBytes>(dimg, col_w + 16 * f, kk, lane);
+      }
+    }
   };
   auto wait_step = [&](Frags &F) {
     __builtin_amdgcn_sched_barrier(0);
@@ -479,17 +433,24 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
     __builtin_amdgcn_sched_barrier(0);
   };
-  // MFMA unit m of the order (kk, a, b).
-  constexpr int kNMfma = kKK * kFM * kFN;
-  auto mfma_one = [&](Frags &F, int m) {
-    const int kk = m / (kFM * kFN);
-    const int a = (m / kFN) % kFM;
-    const int b = m % kFN;
+  auto mfma_step = [&](Frags &F) {
     if constexpr ((SPUTNIK_EXP & 1) != 0) {
-      asm volatile("" ::"v"(F.a[kk][a]), "v"(F.b[kk][b]));
+#pragma unroll
+      for (int kk = 0; kk < kKK; ++kk) {
+#pragma unroll
+        for (int a = 0; a < kFM; ++a) asm volatile("" ::"v"(F.a[kk][a]));
+#pragma unroll
+        for (int b = 0; b < kFN; ++b) asm volatile("" ::"v"(F.b[kk][b]));
+      }
       return;
     }
-    acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
+#pragma unroll
+    for (int kk = 0; kk < kKK; ++kk)
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b)
+          acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
   };
 
   // Software pipeline over k-steps [first, first + steps) (issue() indices).
@@ -498,29 +459,17 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   //   1. waits for its own DMA of step i+1 (counted vmcnt: i+2 stays in
   //      flight) and meets the other waves at a raw s_barrier, after which
   //      step i+1's slot is complete and step i's slot is no longer read;
-  //   2. in kNG groups pinned by sched_barrier, interleaves the refill of
-  //      step i's slot (DMA of step i+3), the LDS reads of step i+1 into
-  //      `next` and the MFMAs of step i on `cur`, so DMA and read issue
-  //      overlap the matrix pipe instead of preceding it;
-  //   3. waits for `next`.
-  // The sparse index entry of step i+3 was read from LDS during step i-1
-  // (pf_*), so no LDS round trip sits between the barrier and the DMA.
-  // The ring is fully drained on return.
-  // flush_at > 0: after the MFMAs of step flush_at - 1 the accumulators are
-  // handed to flush() and restarted from zero; the DMA ring keeps streaming.
-  constexpr int kNG = 8;                              // groups per step
-  constexpr int kReadGroups = kNG - 2;                // reads land early
-  constexpr int kReadsPerGroup = (kNRead + kReadGroups - 1) / kReadGroups;
-  constexpr int kDmaPerGroup = (kNDma + kNG - 1) / kNG;
-  static_assert(kNMfma % kNG == 0, "MFMA groups");
-  constexpr int kMfmaPerGroup = kNMfma / kNG;
-  auto pipeline = [&](int first, int steps, int flush_at, auto &&flush) {
+  //   2. refills step i's slot with the DMA of step i+3;
+  //   3. issues the LDS reads of step i+1 into `next` and, without waiting for
+  //      them, the MFMAs of step i on `cur`;
+  //   4. waits for `next`.
+  // DMA therefore has two steps of MFMA time to land and the LDS read latency
+  // hides under the MFMAs. The ring is fully drained on return.
+  auto pipeline = [&](int first, int steps) {
     if (steps <= 0) return;
     issue(first, 0);
     if (steps > 1) issue(first + 1, 1);
     if (steps > 2) issue(first + 2, 2);
-    int pf_kc = 0, pf_blk = 0;  // index entry of step first+3
-    if (steps > 3) step_index(first + 3, pf_kc, pf_blk);
     if (steps > 2)
       wait_vmcnt<2 * kGroup>();
     else if (steps > 1)
@@ -534,54 +483,17 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     int slot = 0;  // slot of step i
     auto body = [&](int i, Frags &cur, Frags &next) {
       const int nslot = slot + 1 == kStages ? 0 : slot + 1;
-      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-      if constexpr ((SPUTNIK_EXP & 128) != 0) t0 = __builtin_amdgcn_s_memtime();
-      const bool more = i + 1 < steps;
-      const bool refill = i + 3 < steps;
-      if (more) {
+      if (i + 1 < steps) {
         if (i + 2 < steps)
           wait_vmcnt<kGroup>();
         else
           wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
+        if (i + 3 < steps) issue(first + i + 3, slot);
+        read_step(nslot, next);
       }
-      if constexpr ((SPUTNIK_EXP & 128) != 0) t1 = __builtin_amdgcn_s_memtime();
-      IssueCtx c{};
-      if (refill)
-        c = prep_issue(first + i + 3, slot,
-                       __builtin_amdgcn_readfirstlane(pf_kc),
-                       __builtin_amdgcn_readfirstlane(pf_blk));
-      if constexpr ((SPUTNIK_EXP & 128) != 0) t2 = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int g = 0; g < kNG; ++g) {
-        if (refill) {
-#pragma unroll
-          for (int q = g * kDmaPerGroup; q < (g + 1) * kDmaPerGroup; ++q)
-            if (q < kNDma) issue_one(c, q);
-          if (g == 0 && i + 4 < steps)
-            step_index(first + i + 4, pf_kc, pf_blk);
-        }
-        if (more && g < kReadGroups) {
-#pragma unroll
-          for (int u = g * kReadsPerGroup; u < (g + 1) * kReadsPerGroup; ++u)
-            if (u < kNRead) read_one(nslot, next, u);
-        }
-#pragma unroll
-        for (int m = g * kMfmaPerGroup; m < (g + 1) * kMfmaPerGroup; ++m)
-          mfma_one(cur, m);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr ((SPUTNIK_EXP & 128) != 0) t3 = __builtin_amdgcn_s_memtime();
-      if (more) wait_step(next);
-      if constexpr ((SPUTNIK_EXP & 128) != 0) {
-        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
-        acct[0] += t1 - t0;  // vmcnt wait + barrier
-        acct[1] += t2 - t1;  // DMA descriptor setup
-        acct[2] += t3 - t2;  // interleaved DMA / read / MFMA issue
-        acct[4] += t4 - t3;  // fragment-read wait
-      }
-      if (i + 1 == flush_at) flush();
+      mfma_step(cur);
+      if (i + 1 < steps) wait_step(next);
       slot = nslot;
     };
     for (int i = 0; i < steps; i += 2) {
@@ -608,7 +520,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       __syncthreads();
       const int lo = max(s_begin, cb * kStepsPerBlock);
       const int hi = min(s_end, (cb + n) * kStepsPerBlock);
-      pipeline(lo - cb * kStepsPerBlock, hi - lo, -1, [] {});
+      pipeline(lo - cb * kStepsPerBlock, hi - lo);
     }
   };
 
@@ -686,154 +598,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
   };
 
-  // Block-row ranking for the sparse-row products: rank_rows(ra, rb) finds
-  // the rows of rank ra and rb (rank 0 = most nonzeros, ties by row index)
-  // with one parallel pass over the offsets staged in LDS (R <= kLptRows).
-  // Returns {row_a, row_b}; the LDS ring is free again on return.
-  auto rank_rows = [&](int ra, int rb) {
-    const int R = p.num_rows;
-    int *offs = reinterpret_cast<int *>(lds);
-    for (int r = tid; r <= R; r += kThreads) offs[r] = p.s_offsets[r];
-    __syncthreads();
-    for (int r = tid; r < R; r += kThreads) {
-      const int nr = offs[r + 1] - offs[r];
-      int rank = 0;
-      for (int r2 = 0; r2 < R; ++r2) {
-        const int n2 = offs[r2 + 1] - offs[r2];
-        rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
-      }
-      if (rank == ra) scratch[0] = r;
-      if (rank == rb) scratch[1] = r;
-    }
-    __syncthreads();
-    const int row_a = __builtin_amdgcn_readfirstlane(scratch[0]);
-    const int row_b = __builtin_amdgcn_readfirstlane(scratch[1]);
-    __syncthreads();
-    return make_int2(row_a, row_b);
-  };
-
-  long long out_block = 0;
-  if (!kSparseOut && p.pair) {
-    // ==== pair balancing (sparse-row products, #tiles <= resident WGs) ====
-    // A tile's length is its block-row's nonzero count, so one tile per
-    // workgroup finishes when the longest row does. Within each panel the
-    // rows are paired by rank, i <-> R-1-i; the heavy row (rank i, n_h
-    // blocks) gives its first hb = (n_h - n_l) / 2 blocks to the light row's
-    // workgroup (rank R-1-i, n_l blocks), which runs them first in the same
-    // pipeline, stores the fp32 partial (sc1) and raises the pair's flag;
-    // the heavy workgroup runs blocks [hb, n_h), waits for the flag and adds
-    // the partial. Both then run (n_h + n_l) / 2 blocks, +-1. Grid order:
-    // [light x P*(R/2)] [middle row of odd R x P] [heavy x P*(R/2)], so a
-    // producer always precedes its consumer in dispatch order and never
-    // waits. Light and heavy halves use the same XCD-aware map, so a pair
-    // shares an XCD whenever P*(R/2) + P*(R&1) is a multiple of 8.
-    const int R = p.num_rows;
-    const int half = R >> 1;
-    const int n_light = p.num_jtiles * half;
-    const int n_solo = p.num_jtiles * (R & 1);
-    const int bid = blockIdx.x;
-    int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
-    if (bid < n_light) {
-      role = 0;
-      const int t = xcd_tile(bid, n_light);
-      panel = t / half;
-      pi = t % half;
-    } else if (bid < n_light + n_solo) {
-      role = 1;
-      panel = bid - n_light;
-      pi = half;
-    } else {
-      role = 2;
-      const int t = xcd_tile(bid - n_light - n_solo, n_light);
-      panel = t / half;
-      pi = t % half;
-    }
-    const int2 rows = rank_rows(pi, R - 1 - pi);
-    const int e_h = p.s_offsets[rows.x];
-    const int n_h = p.s_offsets[rows.x + 1] - e_h;
-    const int e_l = p.s_offsets[rows.y];
-    const int n_l = p.s_offsets[rows.y + 1] - e_l;
-    const int hb = role == 1 ? 0 : (n_h - n_l) >> 1;
-    const int pair_id = panel * half + pi;
-    j0 = panel * kBN;
-    setup_d(j0);
-    zero_acc();
-    // Partial layout: fragment (a, b) of lane l in the pair's slot at
-    // slot + lane_base + (a*kFN + b) KiB; one 1 KiB wave-instruction each.
-    const __amdgpu_buffer_rsrc_t rp =
-        make_rsrc(reinterpret_cast<const char *>(p.pair_partials));
-    constexpr int kSlotBytes = kBM * kBN * 4;
-    constexpr int kSc1 = 16;  // cache policy: sc1 (L1 bypass, write-through)
-    const int lane_base = pair_id * kSlotBytes +
-                          (wave * kFM * kFN * 64 + lane) * 16;
-    if (role == 0) {
-      // Producer. Hand-off without fences (MI355X_MICROARCH.md, hand-off
-      // table row 1): every partial byte stored and loaded sc1, each
-      // storing wave drains vmcnt, a barrier, then ONE lane stores the flag
-      // (relaxed, agent scope = sc1).
-      srow = rows.y;
-      __syncthreads();
-      const bool col_order = p.s_block_offsets != nullptr;
-      for (int e = tid; e < hb + n_l; e += kThreads) {
-        const int ge = e < hb ? e_h + e : e_l + (e - hb);
-        idx_kc[e] = p.s_indices[ge];
-        idx_blk[e] = col_order ? p.s_block_offsets[ge] : ge;
-      }
-      __syncthreads();
-      auto publish = [&]() {
-#pragma unroll
-        for (int a = 0; a < kFM; ++a)
-#pragma unroll
-          for (int b = 0; b < kFN; ++b)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                __builtin_bit_cast(v4u, acc[a][b]), rp, lane_base,
-                (a * kFN + b) * 1024, kSc1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (tid == 0)
-          __hip_atomic_store(p.pair_flags + pair_id, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        zero_acc();
-      };
-      exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
-      exp_stamp(p.debug, 7, (hb + n_l) * kStepsPerBlock);
-      pipeline(0, (hb + n_l) * kStepsPerBlock,
-               hb > 0 ? hb * kStepsPerBlock : -1, publish);
-    } else {
-      srow = rows.x;
-      exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
-      exp_stamp(p.debug, 7, (n_h - hb) * kStepsPerBlock);
-      run_sparse(e_h, hb * kStepsPerBlock, n_h * kStepsPerBlock);
-      if (hb > 0) {
-        // Consumer: poll (sc1), barrier, sc1 loads; then reset the flag for
-        // the next launch (stream order makes that reset visible to it).
-        if (tid == 0) {
-          int spins = 0;
-          while (__hip_atomic_load(p.pair_flags + pair_id, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) != 1u &&
-                 spins < kSpinLimit) {
-            __builtin_amdgcn_s_sleep(1);
-            ++spins;
-          }
-          __hip_atomic_store(p.pair_flags + pair_id, 0u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int a = 0; a < kFM; ++a)
-#pragma unroll
-          for (int b = 0; b < kFN; ++b)
-            acc[a][b] += __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                           rp, lane_base, (a * kFN + b) * 1024, kSc1));
-      }
-    }
-    exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
-    write_tile(0);
-  } else {
+  {
     // ==== one output tile per workgroup ===================================
     const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                        : xcd_tile(blockIdx.x, gridDim.x);
+    long long out_block = 0;
     int entry0 = 0, entries = 0;
     if constexpr (kSparseOut) {
       out_block = tile;
@@ -841,17 +610,38 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       j0 = p.c_indices[tile] * kBlock;
     } else {
       // Longest-processing-time order: within each dense panel, tile t takes
-      // the block-row with the t-th most nonzeros, so the workgroups
-      // dispatched last are the shortest (taller matrices, R > kLptRows,
-      // keep natural order: they have many more tiles than CUs).
+      // the block-row with the t-th most nonzeros (ties by row index), so the
+      // workgroups dispatched last are the shortest. Snake: odd panels run
+      // ascending, so two workgroups sharing a CU pair a long row with a
+      // short one. Rows are ranked in LDS (R <= kLptRows; taller matrices
+      // have many more tiles than CUs and keep natural order).
       const int panel = tile / p.num_rows;
-      const int target = tile % p.num_rows;
+      int target = tile % p.num_rows;
+      if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
       j0 = panel * kBN;
       srow = target;
-      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows)
-        srow = rank_rows(target, target).x;
-      entry0 = p.s_offsets[srow];
-      entries = p.s_offsets[srow + 1] - entry0;
+      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
+        int *offs = reinterpret_cast<int *>(lds);
+        for (int r = tid; r <= p.num_rows; r += kThreads)
+          offs[r] = p.s_offsets[r];
+        __syncthreads();
+        for (int r = tid; r < p.num_rows; r += kThreads) {
+          const int nr = offs[r + 1] - offs[r];
+          int rank = 0;
+          for (int r2 = 0; r2 < p.num_rows; ++r2) {
+            const int n2 = offs[r2 + 1] - offs[r2];
+            rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
+          }
+          if (rank == target) scratch[0] = r;
+        }
+        __syncthreads();
+        srow = __builtin_amdgcn_readfirstlane(scratch[0]);
+        entry0 = offs[srow];
+        entries = offs[srow + 1] - entry0;
+      } else {
+        entry0 = p.s_offsets[srow];
+        entries = p.s_offsets[srow + 1] - entry0;
+      }
     }
     setup_d(j0);
     zero_acc();
@@ -859,21 +649,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     if constexpr (kSparseOut) {
       const int nsteps = (p.k_limit + kBK - 1) / kBK;
       exp_stamp(p.debug, 7, nsteps);
-      pipeline(0, nsteps, -1, [] {});
+      pipeline(0, nsteps);
     } else {
       exp_stamp(p.debug, 7, entries * kStepsPerBlock);
       run_sparse(entry0, 0, entries * kStepsPerBlock);
     }
-    exp_stamp(p.debug, 3, __builtin_amdgcn_s_memtime());
+    exp_stamp(p.debug, 3, __builtin_amdgcn_s_memrealtime());
     write_tile(out_block);
   }
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
-  if constexpr ((SPUTNIK_EXP & 128) != 0) {
-    // wave 0's per-phase cycle sums replace the start stamps 0, 5, 6.
-    exp_stamp(p.debug, 0, acct[0]);
-    exp_stamp(p.debug, 5, acct[1] | (acct[2] << 32));
-    exp_stamp(p.debug, 6, acct[3] | (acct[4] << 32));
-  }
 }
 
 // Host-side launch of one instantiation (defined in block_gemm.hip).

@@ -145,8 +145,8 @@ def test_dsd_deterministic():
 
 
 def _skewed_topology(rows_b, cols_b, rng):
-    """Block-rows with very different lengths (0 .. cols_b blocks), so pair
-    balancing hands large heads from heavy to light rows."""
+    """Block-rows with very different lengths (0 .. cols_b blocks): the LPT
+    row ranking and its snake order see every rank."""
     mask = np.zeros((rows_b, cols_b), dtype=bool)
     for r in range(rows_b):
         n = int(rng.integers(0, cols_b + 1))
@@ -158,10 +158,9 @@ def _skewed_topology(rows_b, cols_b, rng):
 
 @pytest.mark.parametrize("op", ["dsd", "dds"])
 @pytest.mark.parametrize("rows_b", [2, 7, 32])
-def test_pair_balancing_skewed_rows(op, rows_b):
-    """Skewed row lengths through the pair-balanced schedule (every tile
-    resident): DSD NN and DDS NT (row-order S) and their column-order
-    variants, odd row counts (unpaired middle row), empty rows."""
+def test_skewed_row_lengths(op, rows_b):
+    """Skewed row lengths: DSD NN and DDS NT (row-order S) and their
+    column-order variants, odd row counts, empty and full rows."""
     rng = np.random.default_rng(rows_b)
     kb = 24
     for t in (False, True):
@@ -204,16 +203,16 @@ def test_pair_balancing_skewed_rows(op, rows_b):
         H.assert_close(c_t.float().cpu().numpy(), ref, "f16", f"{op} t={t}")
 
 
-def test_pair_balancing_graph_replay():
-    """The hand-off flags are reset inside each launch, so a captured launch
-    replays correctly (and repeated launches agree bit for bit)."""
+def test_graph_replay():
+    """A launch captured into a HIP graph (torch.cuda.graph on a side stream)
+    replays bit-identically to the eager launch."""
     rng = np.random.default_rng(9)
     off, idx = _skewed_topology(16, 16, rng)
     A = H.HostSparse(2048, 2048, int(off[-1]) * 16384, rng,
                      topology=(off, idx))
     B = H.HostDense(2048, 1024, rng)
     C, c_t = H.empty_dense(2048, 1024)
-    sp.Matmul(A.matrix, False, B.matrix, False, C)  # workspace allocated
+    sp.Matmul(A.matrix, False, B.matrix, False, C)
     _sync()
     first = c_t.clone()
     ref = O.gemm(A.dense(), False, B.values, False, a_mask=A.mask(),
@@ -222,7 +221,7 @@ def test_pair_balancing_graph_replay():
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
-        sp.Matmul(A.matrix, False, B.matrix, False, C)  # this stream's slot
+        sp.Matmul(A.matrix, False, B.matrix, False, C)
     torch.cuda.current_stream().wait_stream(s)
     _sync()
     g = torch.cuda.CUDAGraph()
