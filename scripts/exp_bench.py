@@ -23,18 +23,40 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--op", default="dsd", choices=["dsd", "sdd", "moe_sdd", "moe_dsd"])
     args = ap.parse_args()
     import torch
     import bench
     torch.cuda.set_device(0)
-    prob = bench.Problem(args.m, args.k, args.n, args.density, args.dtype, 0,
-                         torch.device("cuda", 0))
-    ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
+    dev = torch.device("cuda", 0)
+    if args.op == "dsd":
+        prob = bench.Problem(args.m, args.k, args.n, args.density, args.dtype, 0, dev)
+        ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
+        fname = "sputnik_dsd_ex"
+    elif args.op == "sdd":
+        prob = bench.PairProblem(args.k, args.density, args.dtype, 0, dev)
+        import sputnik_amd as sp
+        d = args.k
+        ca, cb = sp.Matrix(d, d, prob.x)._c(), sp.Matrix(d, d, prob.w)._c()
+        cc = prob.C._c()
+        prob.flops = prob.flops / 2
+        fname = "sputnik_sdd"
+    else:
+        prob = bench.MoeProblem("bf16", 0, dev)
+        import sputnik_amd as sp
+        t, dm, cols = prob.dims
+        prob.flops = prob.flops / 2
+        if args.op == "moe_sdd":
+            ca, cb, cc = sp.Matrix(t, dm, prob.x)._c(), sp.Matrix(dm, cols, prob.w1)._c(), prob.H._c()
+            fname = "sputnik_sdd"
+        else:
+            ca, cb, cc = prob.H._c(), sp.Matrix(cols, dm, prob.w2)._c(), sp.Matrix(t, dm, prob.y)._c()
+            fname = "sputnik_dsd_ex"
     stream = torch.cuda.current_stream().cuda_stream
     fns = []
     for path in args.libs:
         L = ctypes.CDLL(os.path.abspath(path))
-        fn = L.sputnik_dsd_ex
+        fn = getattr(L, fname)
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                        ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                        ctypes.c_void_p]
@@ -63,7 +85,7 @@ def main():
         med = statistics.median(t)
         out[n] = {"us_median": round(med, 2), "us_min": round(min(t), 2),
                   "tflops": round(prob.flops / (med * 1e-6) / 1e12, 1)}
-    print(json.dumps({"density": args.density, "m": args.m, "k": args.k,
+    print(json.dumps({"op": args.op, "density": args.density, "m": args.m, "k": args.k,
                       "n": args.n, "results": out}))
 
 

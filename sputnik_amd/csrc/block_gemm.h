@@ -56,7 +56,7 @@ namespace sputnik_amd {
 
 constexpr int kBlock = 128;        // BCSR block edge (only 128 is supported)
 constexpr int kBM = 128;           // output tile rows = one sparse block-row
-constexpr int kIndexChunk = 1024;  // sparse-row entries staged in LDS at once
+constexpr int kMaxIndexChunk = 1024;  // sparse-row entries staged in LDS at once
 constexpr int kLptRows = 256;      // rank block-rows in-kernel up to this many
 constexpr uint32_t kOOB = 0x80000000u;      // buffer offset that reads as 0
 constexpr uint32_t kNumRecords = 0x7fffffffu;
@@ -228,11 +228,20 @@ using CfgWide512 = TileConfig<512, 1, 4, 32, 3, 1>;
 using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
+// 128x128 tile, 4 waves of 64x64, BK=32, three workgroups per CU (12 waves:
+// three per SIMD to hide each wave's DMA/read issue chain).
+using CfgTri = TileConfig<128, 2, 2, 32, 3, 3>;
+// Same tile, two workgroups per CU.
+using CfgBlock2 = TileConfig<128, 2, 2, 32, 3, 2>;
 
 #ifndef SPUTNIK_SPARSE_CFG
 #define SPUTNIK_SPARSE_CFG CfgDual
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
+#ifndef SPUTNIK_SDD_CFG
+#define SPUTNIK_SDD_CFG CfgBlock
+#endif
+using CfgSdd = SPUTNIK_SDD_CFG;        // SDD tile configuration (BN = 128)
 
 // kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
@@ -267,6 +276,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr int kDRowsPerInstr = 64 / kDChunksPerRow;
   constexpr int kStepsPerBlock = kBlock / kBK;
   constexpr int kRingBytes = kStages * kStageBytes;
+  // Index list staged per chunk: smaller when three workgroups share a CU.
+  constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
   constexpr int kIdxBytes = kSparseOut ? 16 : kIndexChunk * 6 + 16;
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
@@ -353,6 +364,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // Issue the DMA of pipeline step `step` into ring slot `slot`. Sparse S:
   // `step` counts from the first entry staged in the LDS index list.
   int srow = 0, j0 = 0;  // current tile
+  // Sparse S: the entry's block bases are cached across the kStepsPerBlock
+  // steps of one block, so the LDS index lookup (a serialized LDS round
+  // trip before the DMA) happens once per block, not once per step.
+  int cached_e = -1;
+  const char *blk_s = nullptr;
+  const char *blk_d = nullptr;
   auto issue = [&](int step, int slot) {
     if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
@@ -369,13 +386,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     } else {
       const int e = step / kStepsPerBlock;
       const int h = step % kStepsPerBlock;
-      const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
-      const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
-      s_base = p.s_data + (long long)blk * (kBlock * kBlock * 2) +
-               (kSKC ? h * (kBK * 2) : h * (kBK * 256));
-      const long long kg = (long long)kblk * kBlock + h * kBK;
-      d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
-                    : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+      if (e != cached_e) {
+        cached_e = e;
+        const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
+        const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
+        blk_s = p.s_data + (long long)blk * (kBlock * kBlock * 2);
+        const long long kg = (long long)kblk * kBlock;
+        blk_d = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
+                     : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+      }
+      s_base = blk_s + (kSKC ? h * (kBK * 2) : h * (kBK * 256));
+      d_base = blk_d + (kDKC ? (long long)h * (kBK * 2)
+                             : (long long)h * kBK * p.d_ld);
     }
     char *slot_base = lds + slot * kStageBytes;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(s_base);
@@ -444,6 +466,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       }
       return;
     }
+#if SPUTNIK_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int kk = 0; kk < kKK; ++kk)
 #pragma unroll
@@ -451,6 +476,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 #pragma unroll
         for (int b = 0; b < kFN; ++b)
           acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
+#if SPUTNIK_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   };
 
   // Software pipeline over k-steps [first, first + steps) (issue() indices).
@@ -520,6 +548,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       __syncthreads();
       const int lo = max(s_begin, cb * kStepsPerBlock);
       const int hi = min(s_end, (cb + n) * kStepsPerBlock);
+      cached_e = -1;
       pipeline(lo - cb * kStepsPerBlock, hi - lo);
     }
   };

@@ -13,8 +13,7 @@ namespace {
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT>
 hipError_t Launch(const GemmParams &p, hipStream_t stream) {
   if (p.num_tiles <= 0) return hipSuccess;
-  using Cfg = typename std::conditional<kSparseOut, CfgBlock,
-                                        CfgSparse>::type;
+  using Cfg = typename std::conditional<kSparseOut, CfgSdd, CfgSparse>::type;
   hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, Cfg>),
                      dim3(p.num_tiles), dim3(64 * Cfg::kWM * Cfg::kWN), 0,
                      stream, p);
