@@ -18,8 +18,11 @@ R=$GRAFT_REPO_ROOT
       python3 $R/bench.py --steps 20 --warmup 3 --sweep "" --no-cpu > $R/$OUT/pmc_p$i.log 2>&1 || exit $?
   done ); rc=$?; echo "== pmc rc=$rc" | tee -a $OUT/steps.log; fatal $rc && exit $rc
 python scripts/pmc_traffic.py $OUT/pmc dsd_4096x4096x4096_0.5_f16 $OUT/pmc_latest.json
-step bench 600 python bench.py --steps 100 --warmup 10 --pmc $OUT/pmc_latest.json; rc=$?; fatal $rc && exit $rc
+step bench 600 python bench.py --pmc $OUT/pmc_latest.json; rc=$?; fatal $rc && exit $rc
 ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d $R/$OUT/prof -o run -- \
-    python3 $R/bench.py --steps 100 --warmup 10 --sweep "" --no-cpu --pmc $R/$OUT/pmc_latest.json > $R/$OUT/prof.log 2>&1 ); rc=$?
-echo "== prof rc=$rc" | tee -a $OUT/steps.log
-exit $rc
+    python3 $R/bench.py --sweep "" --no-cpu --pmc $R/$OUT/pmc_latest.json > $R/$OUT/prof.log 2>&1 ); rc=$?
+echo "== prof rc=$rc" | tee -a $OUT/steps.log; fatal $rc && exit $rc
+for w in sdd_dds moe panel; do
+  step bench_$w 300 python bench.py --workload $w; rc=$?; fatal $rc && exit $rc
+done
+exit 0
