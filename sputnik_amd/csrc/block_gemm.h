@@ -66,6 +66,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 #define SPUTNIK_LDS(p) ((__attribute__((address_space(3))) void *)(p))
 #define SPUTNIK_LDS_S4(p) ((__attribute__((address_space(3))) s16x4 *)(p))
@@ -88,6 +89,14 @@ struct GemmParams {
   int j_limit;                 // dense extent (elements) of the j dimension
   int k_limit;                 // SDD: K (elements)
   int num_tiles;               // output tiles (one-tile-per-workgroup grid)
+  // Pair balancing (staggered one-workgroup-per-CU configs, see the
+  // kernel): the block-rows of each panel are paired heaviest-with-lightest;
+  // the light workgroup also computes the head of the heavy row and hands it
+  // over as an fp32 partial. pair == 0: one tile per workgroup, LPT order.
+  int pair;
+  float *pair_partials;        // (#pairs) x (128 x BN) fp32
+  unsigned *pair_flags;        // #pairs; 1 = partial published, reset to 0
+                               // by the consumer (graph-replay safe)
   unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
 };
 
@@ -132,6 +141,19 @@ __device__ __forceinline__ void wait_vmcnt() {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const char *base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0,
                                            kNumRecords, 0x00020000);
+}
+
+// Wave-uniform loads through the scalar cache (s_load_dword): the sparse
+// index list is read-only for the whole launch. An int16 entry is taken from
+// its aligned dword, so any 2-byte-aligned base works.
+__device__ __forceinline__ int scalar_load_short(const short *base, int e) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base + e);
+  const int v = *reinterpret_cast<const __attribute__((address_space(4))) int *>(
+      a & ~uintptr_t(3));
+  return ((a & 2) ? (v >> 16) : v) & 0xffff;
+}
+__device__ __forceinline__ int scalar_load_int(const int *base, int e) {
+  return *(const __attribute__((address_space(4))) int *)(base + e);
 }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds_dst,
@@ -206,16 +228,22 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
 // depth of one LDS ring slot; kWGs workgroups are meant to share a CU (it
 // sets the register budget through __launch_bounds__ and must match the LDS
 // footprint).
-template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_>
+template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_,
+          int STAGGER_ = 0>
 struct TileConfig {
   static constexpr int kBN = BN_, kWM = WM_, kWN = WN_, kBK = BK_;
   static constexpr int kStages = STAGES_, kWGs = WGS_;
+  // kStagger: the two halves of the waves (wave w and w + kNW/2 share a
+  // SIMD) run one barrier apart, so one half's DMA/read phase overlaps the
+  // other half's MFMA phase (needs kStages >= 4; see the pipeline).
+  static constexpr bool kStagger = STAGGER_ != 0;
 };
 
 // 8 waves, 64x64 each, BK=64, one workgroup per CU (first-generation DSD/DDS).
 using CfgWide = TileConfig<256, 2, 4, 64, 3, 1>;
 // 4 waves, 64x128 each, BK=32, two workgroups per CU: 25% fewer LDS fragment
-// bytes per MFMA than CfgWide and two independent barrier domains per CU.
+// bytes per MFMA than CfgWide and two independent barrier domains per CU
+// (the r01 default before CfgWide8S).
 using CfgDual = TileConfig<256, 2, 2, 32, 3, 2>;
 // 2 waves of 128x128 (one per SIMD, 512-register budget), BK=32, two
 // workgroups per CU (measured slower than CfgDual: DESIGN.md §10).
@@ -226,6 +254,10 @@ using CfgWide512 = TileConfig<512, 1, 4, 32, 3, 1>;
 // 128x512 tile, 8 waves of 64x128, BK=32, one workgroup per CU (measured
 // slower than CfgDual without cross-workgroup balancing: DESIGN.md §10).
 using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
+// DSD/DDS default: CfgWide8 with staggered wave halves and a 4-slot ring
+// (the whole 160 KiB LDS; the sparse index list is then read with scalar
+// loads, not staged), pair-balanced across block-rows (dispatch.cpp).
+using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 // 128x128 tile, 4 waves of 64x64, BK=32, three workgroups per CU (12 waves:
@@ -235,13 +267,19 @@ using CfgTri = TileConfig<128, 2, 2, 32, 3, 3>;
 using CfgBlock2 = TileConfig<128, 2, 2, 32, 3, 2>;
 
 #ifndef SPUTNIK_SPARSE_CFG
-#define SPUTNIK_SPARSE_CFG CfgDual
+#define SPUTNIK_SPARSE_CFG CfgWide8S
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
 #ifndef SPUTNIK_SDD_CFG
 #define SPUTNIK_SDD_CFG CfgBlock
 #endif
 using CfgSdd = SPUTNIK_SDD_CFG;        // SDD tile configuration (BN = 128)
+
+// Bounded spin for the pair hand-off (about 0.1 s): a launch can never hang
+// on a missing partial. The producer never waits and always has a lower
+// workgroup index than its consumer (in-order dispatch), so the bound is a
+// guard, not part of the protocol.
+constexpr int kSpinLimit = 1 << 22;
 
 // kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
@@ -276,9 +314,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr int kDRowsPerInstr = 64 / kDChunksPerRow;
   constexpr int kStepsPerBlock = kBlock / kBK;
   constexpr int kRingBytes = kStages * kStageBytes;
-  // Index list staged per chunk: smaller when three workgroups share a CU.
+  // Index list staged per chunk in LDS (smaller when three workgroups share
+  // a CU); staggered configs read it with scalar loads instead.
+  constexpr bool kScalarIdx = Cfg::kStagger;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
-  constexpr int kIdxBytes = kSparseOut ? 16 : kIndexChunk * 6 + 16;
+  constexpr int kIdxBytes =
+      kSparseOut ? 16 : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
+  static_assert(!Cfg::kStagger || kStages >= 4, "stagger needs 4 slots");
+  static_assert(!Cfg::kStagger || (Cfg::kWM * Cfg::kWN) % 2 == 0, "halves");
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
   static_assert(kTM % 16 == 0 && kTN % 16 == 0 && kBK % 32 == 0, "tiles");
@@ -289,7 +332,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   __shared__ __attribute__((aligned(1024))) char lds[kRingBytes + kIdxBytes];
   short *idx_kc = reinterpret_cast<short *>(lds + kRingBytes);
   int *idx_blk = reinterpret_cast<int *>(lds + kRingBytes + kIndexChunk * 2);
-  int *scratch = reinterpret_cast<int *>(lds + kRingBytes + kIdxBytes - 16);
+  // 4 scratch ints: after the index list, or (scalar-index configs) inside
+  // the ring, which is only used for them before the pipeline starts.
+  int *scratch = reinterpret_cast<int *>(
+      kIdxBytes >= 16 ? lds + kRingBytes + kIdxBytes - 16 : lds + 4096);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -368,6 +414,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // steps of one block, so the LDS index lookup (a serialized LDS round
   // trip before the DMA) happens once per block, not once per step.
   int cached_e = -1;
+  // Scalar-index configs: entry e of the pipeline is idx_base + e, or, past
+  // idx_split entries (a pair producer's second segment), idx_base2 + e -
+  // idx_split.
+  int idx_base = 0, idx_split = 0x7fffffff, idx_base2 = 0;
   const char *blk_s = nullptr;
   const char *blk_d = nullptr;
   auto issue = [&](int step, int slot) {
@@ -388,8 +438,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       const int h = step % kStepsPerBlock;
       if (e != cached_e) {
         cached_e = e;
-        const int kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
-        const int blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
+        int kblk, blk;
+        if constexpr (kScalarIdx) {
+          const int ge =
+              e < idx_split ? idx_base + e : idx_base2 + (e - idx_split);
+          kblk = scalar_load_short(p.s_indices, ge);
+          blk = p.s_block_offsets != nullptr
+                    ? scalar_load_int(p.s_block_offsets, ge)
+                    : ge;
+        } else {
+          kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
+          blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
+        }
         blk_s = p.s_data + (long long)blk * (kBlock * kBlock * 2);
         const long long kg = (long long)kblk * kBlock;
         blk_d = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
@@ -493,7 +553,78 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   //   4. waits for `next`.
   // DMA therefore has two steps of MFMA time to land and the LDS read latency
   // hides under the MFMAs. The ring is fully drained on return.
-  auto pipeline = [&](int first, int steps) {
+  // ---- pair hand-off (see the pair branch below) ---------------------------
+  // Partial layout: fragment (a, b) of lane l at pair slot + lane_base +
+  // (a*kFN + b) KiB, one 1 KiB wave-instruction each. Hand-off without
+  // fences (MI355X_MICROARCH.md, hand-off table row 1): every partial byte is
+  // stored and loaded sc1 (L1 bypass, write-through), each storing wave
+  // drains vmcnt before a barrier, then ONE lane stores the flag (relaxed,
+  // agent scope = sc1) and the consumer polls it with sc1 loads.
+  constexpr bool kPairs = kScalarIdx && !kSparseOut;
+  constexpr int kSlotBytes = kBM * kBN * 4;
+  constexpr int kSc1 = 16;  // cache-policy bits: sc1
+  int pair_id = 0;
+  auto pair_rsrc = [&]() {
+    return make_rsrc(reinterpret_cast<const char *>(p.pair_partials));
+  };
+  auto pair_lane_base = [&]() {
+    return pair_id * kSlotBytes + (wave * kFM * kFN * 64 + lane) * 16;
+  };
+  // Called by every wave right after its MFMAs of the last head step. In a
+  // staggered pipeline the lagging half reaches this barrier one barrier
+  // later, so the flag is raised by the last wave (a lagging one): after its
+  // barrier every wave of both halves has drained its stores.
+  auto publish = [&]() {
+    if constexpr (kPairs) {
+      const __amdgpu_buffer_rsrc_t rp = pair_rsrc();
+      const int lb = pair_lane_base();
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b)
+          __builtin_amdgcn_raw_buffer_store_b128(
+              __builtin_bit_cast(v4u, acc[a][b]), rp, lb,
+              (a * kFN + b) * 1024, kSc1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (wave == kNW - 1 && lane == 0)
+        __hip_atomic_store(p.pair_flags + pair_id, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      zero_acc();
+    }
+  };
+  // Consumer side: poll, barrier, add the partial (sc1 loads); the flag is
+  // reset for the next launch (stream order makes the reset visible to it).
+  auto collect = [&]() {
+    if constexpr (kPairs) {
+      if (tid == 0) {
+        int spins = 0;
+        while (__hip_atomic_load(p.pair_flags + pair_id, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) != 1u &&
+               spins < kSpinLimit) {
+          __builtin_amdgcn_s_sleep(1);
+          ++spins;
+        }
+        __hip_atomic_store(p.pair_flags + pair_id, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rp = pair_rsrc();
+      const int lb = pair_lane_base();
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b)
+          acc[a][b] += __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                         rp, lb, (a * kFN + b) * 1024, kSc1));
+    }
+  };
+
+  // flush_at > 0: after the MFMAs of step flush_at - 1 the accumulators are
+  // published (pair producer) and restarted from zero; the ring keeps
+  // streaming.
+  auto pipeline = [&](int first, int steps, int flush_at = -1) {
     if (steps <= 0) return;
     issue(first, 0);
     if (steps > 1) issue(first + 1, 1);
@@ -508,26 +639,68 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     Frags f0, f1;
     read_step(0, f0);
     wait_step(f0);
+    // Staggered configs: the lagging half (waves kNW/2..) passes one barrier
+    // behind the leading half, and every step has two barriers, B1 before
+    // the DMA/read phase and B2 before the MFMA phase, so a lagging wave's
+    // B1 is a leading wave's B2: one half streams while the other computes.
+    // Ordering (4-slot ring, DMA of step i+3 issued after B1(i)):
+    //  - RAW: a wave reads slot i+1 after its B1(i). Leaders wait for their
+    //    own DMA of step i+1 before B1(i); laggers wait for theirs before
+    //    B2(i-1), which is the leaders' B1(i). So every piece of slot i+1 has
+    //    landed before either half reads it.
+    //  - WAR: DMA(i+3) refills slot (i+3)%4 = (i-1)%4, last read during step
+    //    i-2 and drained (lgkmcnt(0)) before each wave's next barrier, which
+    //    precedes both halves' B1(i).
+    // Every wave executes the same number of barriers: laggers add one after
+    // the prologue, leaders one after the loop.
+    const bool lag = Cfg::kStagger && wave >= kNW / 2;
+    if (lag) {
+      if (steps > 2)
+        wait_vmcnt<kGroup>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+    }
     int slot = 0;  // slot of step i
     auto body = [&](int i, Frags &cur, Frags &next) {
       const int nslot = slot + 1 == kStages ? 0 : slot + 1;
       if (i + 1 < steps) {
-        if (i + 2 < steps)
-          wait_vmcnt<kGroup>();
-        else
-          wait_vmcnt<0>();
+        if (!lag) {
+          if (i + 2 < steps)
+            wait_vmcnt<kGroup>();
+          else
+            wait_vmcnt<0>();
+        }
         __builtin_amdgcn_s_barrier();
-        if (i + 3 < steps) issue(first + i + 3, slot);
+        if (i + 3 < steps) {
+          int dslot = slot + 3;
+          if (dslot >= kStages) dslot -= kStages;
+          issue(first + i + 3, dslot);
+        }
         read_step(nslot, next);
+      }
+      if constexpr (Cfg::kStagger) {
+        if (lag) {
+          // Own DMA of step i+2 lands before the leaders read it (B1(i+1)).
+          if (i + 3 < steps)
+            wait_vmcnt<kGroup>();
+          else if (i + 2 < steps)
+            wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
       }
       mfma_step(cur);
       if (i + 1 < steps) wait_step(next);
+      if constexpr (kPairs) {
+        if (i + 1 == flush_at) publish();
+      }
       slot = nslot;
     };
     for (int i = 0; i < steps; i += 2) {
       body(i, f0, f1);
       if (i + 1 < steps) body(i + 1, f1, f0);
     }
+    if (Cfg::kStagger && !lag) __builtin_amdgcn_s_barrier();
   };
 
   // Steps [s_begin, s_end) of sparse block-row `srow` whose entries start at
@@ -627,65 +800,147 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
   };
 
-  {
+  // Rows of rank ra and rb (rank 0 = most nonzeros, ties by row index), one
+  // parallel pass over the offsets staged in LDS (R <= kLptRows). The ring
+  // is free again on return.
+  auto rank_rows = [&](int ra, int rb) {
+    const int R = p.num_rows;
+    int *offs = reinterpret_cast<int *>(lds);
+    for (int r = tid; r <= R; r += kThreads) offs[r] = p.s_offsets[r];
+    __syncthreads();
+    for (int r = tid; r < R; r += kThreads) {
+      const int nr = offs[r + 1] - offs[r];
+      int rank = 0;
+      for (int r2 = 0; r2 < R; ++r2) {
+        const int n2 = offs[r2 + 1] - offs[r2];
+        rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
+      }
+      if (rank == ra) scratch[0] = r;
+      if (rank == rb) scratch[1] = r;
+    }
+    __syncthreads();
+    const int row_a = __builtin_amdgcn_readfirstlane(scratch[0]);
+    const int row_b = __builtin_amdgcn_readfirstlane(scratch[1]);
+    __syncthreads();
+    return make_int2(row_a, row_b);
+  };
+
+  // ---- which work this workgroup does ----------------------------------
+  // Every branch below only sets up (srow, j0, the index segments, the step
+  // range); the pipeline is then entered from ONE call site per kernel, so
+  // it is inlined and the accumulators stay in registers.
+  long long out_block = 0;
+  int entry0 = 0, entries = 0;   // sparse S: the row's CSR entry range
+  int p_first = 0, p_steps = 0;  // scalar-index pipeline range
+  int p_flush = -1;              // pair producer: end of the head segment
+  bool do_collect = false;       // pair consumer
+  bool use_pairs = false;
+  if constexpr (kPairs) use_pairs = p.pair != 0;
+  if (use_pairs) {
+    // ==== pair balancing (one workgroup per CU, #tiles <= #CUs) ==========
+    // A tile's length is its block-row's nonzero count, and with one tile
+    // per CU the launch ends with the longest row. Within each panel the
+    // rows are paired by rank, i <-> R-1-i: the heavy row (rank i, n_h
+    // blocks) gives its first hb = (n_h - n_l) / 2 blocks to the light row's
+    // workgroup (n_l blocks), which runs them first in the same pipeline,
+    // publishes the fp32 partial and then runs its own row; the heavy
+    // workgroup runs blocks [hb, n_h) and adds the partial. Both run
+    // (n_h + n_l) / 2 blocks, +-1. Grid order: [light x P*(R/2)] [middle row
+    // of odd R x P] [heavy x P*(R/2)], so a producer always precedes its
+    // consumer in dispatch order and never waits; pairs share an XCD when
+    // P*(R/2) + P*(R&1) is a multiple of 8.
+    const int R = p.num_rows;
+    const int half = R >> 1;
+    const int n_light = p.num_jtiles * half;
+    const int n_solo = p.num_jtiles * (R & 1);
+    const int bid = blockIdx.x;
+    int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
+    if (bid < n_light) {
+      role = 0;
+      const int t = xcd_tile(bid, n_light);
+      panel = t / half;
+      pi = t % half;
+    } else if (bid < n_light + n_solo) {
+      role = 1;
+      panel = bid - n_light;
+      pi = half;
+    } else {
+      role = 2;
+      const int t = xcd_tile(bid - n_light - n_solo, n_light);
+      panel = t / half;
+      pi = t % half;
+    }
+    const int2 rows = rank_rows(pi, R - 1 - pi);
+    const int e_h = p.s_offsets[rows.x];
+    const int n_h = p.s_offsets[rows.x + 1] - e_h;
+    const int e_l = p.s_offsets[rows.y];
+    const int n_l = p.s_offsets[rows.y + 1] - e_l;
+    const int hb = role == 1 ? 0 : (n_h - n_l) >> 1;
+    pair_id = panel * half + pi;
+    j0 = panel * kBN;
+    if (role == 0) {
+      srow = rows.y;
+      idx_base = e_h;
+      idx_split = hb;
+      idx_base2 = e_l;
+      p_first = 0;
+      p_steps = (hb + n_l) * kStepsPerBlock;
+      p_flush = hb > 0 ? hb * kStepsPerBlock : -1;
+    } else {
+      srow = rows.x;
+      idx_base = e_h;
+      p_first = hb * kStepsPerBlock;
+      p_steps = (n_h - hb) * kStepsPerBlock;
+      do_collect = hb > 0;
+    }
+  } else {
     // ==== one output tile per workgroup ===================================
     const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                        : xcd_tile(blockIdx.x, gridDim.x);
-    long long out_block = 0;
-    int entry0 = 0, entries = 0;
     if constexpr (kSparseOut) {
       out_block = tile;
       srow = p.c_row_indices[tile];
       j0 = p.c_indices[tile] * kBlock;
     } else {
       // Longest-processing-time order: within each dense panel, tile t takes
-      // the block-row with the t-th most nonzeros (ties by row index), so the
-      // workgroups dispatched last are the shortest. Snake: odd panels run
-      // ascending, so two workgroups sharing a CU pair a long row with a
-      // short one. Rows are ranked in LDS (R <= kLptRows; taller matrices
-      // have many more tiles than CUs and keep natural order).
+      // the block-row with the t-th most nonzeros (ties by row index), so
+      // the workgroups dispatched last are the shortest. Snake (several
+      // workgroups per CU): odd panels run ascending, so two workgroups
+      // sharing a CU pair a long row with a short one. Rows are ranked in
+      // LDS (R <= kLptRows; taller matrices have many more tiles than CUs and
+      // keep natural order).
       const int panel = tile / p.num_rows;
       int target = tile % p.num_rows;
       if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
       j0 = panel * kBN;
       srow = target;
-      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
-        int *offs = reinterpret_cast<int *>(lds);
-        for (int r = tid; r <= p.num_rows; r += kThreads)
-          offs[r] = p.s_offsets[r];
-        __syncthreads();
-        for (int r = tid; r < p.num_rows; r += kThreads) {
-          const int nr = offs[r + 1] - offs[r];
-          int rank = 0;
-          for (int r2 = 0; r2 < p.num_rows; ++r2) {
-            const int n2 = offs[r2 + 1] - offs[r2];
-            rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
-          }
-          if (rank == target) scratch[0] = r;
-        }
-        __syncthreads();
-        srow = __builtin_amdgcn_readfirstlane(scratch[0]);
-        entry0 = offs[srow];
-        entries = offs[srow + 1] - entry0;
-      } else {
-        entry0 = p.s_offsets[srow];
-        entries = p.s_offsets[srow + 1] - entry0;
-      }
+      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows)
+        srow = rank_rows(target, target).x;
+      entry0 = p.s_offsets[srow];
+      entries = p.s_offsets[srow + 1] - entry0;
+      idx_base = entry0;
+      p_first = 0;
+      p_steps = entries * kStepsPerBlock;
     }
-    setup_d(j0);
-    zero_acc();
-    exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
-    if constexpr (kSparseOut) {
-      const int nsteps = (p.k_limit + kBK - 1) / kBK;
-      exp_stamp(p.debug, 7, nsteps);
-      pipeline(0, nsteps);
-    } else {
-      exp_stamp(p.debug, 7, entries * kStepsPerBlock);
-      run_sparse(entry0, 0, entries * kStepsPerBlock);
-    }
-    exp_stamp(p.debug, 3, __builtin_amdgcn_s_memrealtime());
-    write_tile(out_block);
   }
+  setup_d(j0);
+  zero_acc();
+  exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
+  if constexpr (kSparseOut) {
+    const int nsteps = (p.k_limit + kBK - 1) / kBK;
+    exp_stamp(p.debug, 7, nsteps);
+    pipeline(0, nsteps);
+  } else if constexpr (kScalarIdx) {
+    exp_stamp(p.debug, 7, p_steps);
+    cached_e = -1;
+    pipeline(p_first, p_steps, p_flush);
+    if (do_collect) collect();
+  } else {
+    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
+    run_sparse(entry0, 0, entries * kStepsPerBlock);
+  }
+  exp_stamp(p.debug, 3, __builtin_amdgcn_s_memrealtime());
+  write_tile(out_block);
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
 }
 

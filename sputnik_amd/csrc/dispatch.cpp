@@ -19,6 +19,7 @@
 // metadata (offsets_t, indices_t, block_offsets), exactly like the reference.
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 
 #include "api_internal.h"
 #include "block_gemm.h"
@@ -30,6 +31,93 @@ namespace sputnik_amd {
 
 // Experiment builds (SPUTNIK_EXP & 16) copy this into GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
+
+// ---- pair-balancing workspace ---------------------------------------------
+// fp32 partial slots + hand-off flags, one set per (device, stream) so
+// concurrent streams never share them. Allocated on the first eligible call
+// and kept for the life of the process (like a BLAS handle's workspace);
+// never allocated while the stream is being captured into a graph (that call
+// runs one tile per workgroup instead). Flags return to 0 inside every
+// launch, so captured launches replay correctly.
+struct PairSlot {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  float *partials = nullptr;
+  unsigned *flags = nullptr;
+  int pairs = 0;  // capacity
+  int slots = 0;  // resident workgroups on the device
+};
+constexpr int kMaxPairSlots = 16;
+static PairSlot g_pairs[kMaxPairSlots];
+static std::mutex g_pairs_mu;
+
+static bool PairsEnabled() {
+#ifdef SPUTNIK_NO_PAIRS
+  return false;
+#endif
+  static const int enabled = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_PAIRS");
+    return e ? std::atoi(e) : 1;
+  }();
+  return enabled != 0;
+}
+
+// Fills the pair fields of p when pair balancing applies: a staggered
+// one-workgroup-per-CU tile config, every tile resident at once (the point
+// is the tail of a single wave of tiles) and rows rankable in-kernel.
+static void PreparePairs(GemmParams *p, hipStream_t stream) {
+  p->pair = 0;
+  if (!CfgSparse::kStagger || CfgSparse::kWGs != 1) return;
+  if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  PairSlot *slot = nullptr;
+  for (auto &s : g_pairs)
+    if (s.partials != nullptr && s.device == dev && s.stream == stream) {
+      slot = &s;
+      break;
+    }
+  if (slot == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+        cs != hipStreamCaptureStatusNone)
+      return;
+    for (auto &s : g_pairs)
+      if (s.partials == nullptr) {
+        slot = &s;
+        break;
+      }
+    if (slot == nullptr) return;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                              dev) != hipSuccess || cus <= 0)
+      return;
+    const int slots = cus * CfgSparse::kWGs;
+    const int pairs = slots / 2;
+    float *partials = nullptr;
+    unsigned *flags = nullptr;
+    if (hipMalloc(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
+                                 sizeof(float)) != hipSuccess)
+      return;
+    if (hipMalloc(&flags, pairs * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(flags, 0, pairs * sizeof(unsigned)) != hipSuccess) {
+      (void)hipFree(partials);
+      if (flags) (void)hipFree(flags);
+      return;
+    }
+    slot->device = dev;
+    slot->stream = stream;
+    slot->partials = partials;
+    slot->flags = flags;
+    slot->pairs = pairs;
+    slot->slots = slots;
+  }
+  if (p->num_tiles > slot->slots) return;
+  p->pair = 1;
+  p->pair_partials = slot->partials;
+  p->pair_flags = slot->flags;
+}
 
 namespace {
 
@@ -218,6 +306,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
+  PreparePairs(&p, stream);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
 }
 
@@ -234,6 +323,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
+  PreparePairs(&p, stream);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, p, stream);
 }
