@@ -83,6 +83,7 @@ struct GemmParams {
   char *c_data;                // output
   long long c_ld;              // dense output row stride in bytes
   const short *c_row_indices;  // SDD: block-row of each output block
+  const int *c_offsets;        // SDD, grouped tiles: C's BCSR row offsets
   const short *c_indices;      // SDD: block-col of each output block
   int num_rows;                // sparse: #block-rows of S
   int num_jtiles;              // sparse: #BN-wide tiles of the dense extent
@@ -260,6 +261,10 @@ using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
+// SDD, grouped: up to 4 consecutive stored blocks of one block-row per
+// workgroup (shared S rows, D columns gathered per lane), on the staggered
+// 128x512 pipeline of CfgWide8S.
+using CfgSddGrouped = TileConfig<512, 2, 4, 32, 4, 1, 1>;
 // 128x128 tile, 4 waves of 64x64, BK=32, three workgroups per CU (12 waves:
 // three per SIMD to hide each wave's DMA/read issue chain).
 using CfgTri = TileConfig<128, 2, 2, 32, 3, 3>;
@@ -319,7 +324,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr bool kScalarIdx = Cfg::kStagger;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
   constexpr int kIdxBytes =
-      kSparseOut ? 16 : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
+      kSparseOut ? (Cfg::kStagger ? 0 : 16)
+                 : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
+  // SDD with kBN > 128: a tile is a group of up to kGrp stored blocks of one
+  // block-row, found in-kernel from C's offsets (rows <= kMaxGroupRows).
+  constexpr bool kGroupedSdd = kSparseOut && kBN > kBlock;
+  constexpr int kGrp = kBN / kBlock;
   static_assert(!Cfg::kStagger || kStages >= 4, "stagger needs 4 slots");
   static_assert(!Cfg::kStagger || (Cfg::kWM * Cfg::kWN) % 2 == 0, "halves");
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
@@ -376,6 +386,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
   }
   // D offsets depend on the tile's dense origin j0 (range mask).
+  // Grouped SDD: block j of the tile (j < grp_count) takes the D columns
+  // grp_col[j] .. +127; lanes of absent blocks read zeros.
+  static_assert(kGrp <= 4, "grouped SDD: at most 4 blocks per tile");
+  long long grp_b0 = 0;   // SDD: first output block of the tile
+  int grp_count = 1;      // SDD: blocks in the tile
+  int grp_c0 = 0, grp_c1 = 0, grp_c2 = 0, grp_c3 = 0;  // D column origins
+  auto grp_col = [&](int jb) {  // lane-dependent select, no private array
+    return jb == 0 ? grp_c0 : jb == 1 ? grp_c1 : jb == 2 ? grp_c2 : grp_c3;
+  };
   auto setup_d = [&](int j0) {
 #pragma unroll
     for (int q = 0; q < kDInstr; ++q) {
@@ -384,16 +403,31 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if constexpr (kDKC) {
         const int j = kKcRowsPerInstr * g + lane / kKcChunks;
         const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(j);
-        d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
+        int n = j0 + j;
+        if constexpr (kGroupedSdd) {
+          const int jb = j / kBlock;
+          n = grp_col(jb) + j % kBlock;
+          ok = jb < grp_count;
+          d_off[q] = (uint32_t)(n * p.d_ld + c * 16);
+        } else {
+          d_off[q] = (uint32_t)(j * p.d_ld + c * 16);
+          ok = n < p.j_limit;
+        }
         d_lk[q] = c * 8;
-        ok = j0 + j < p.j_limit;
       } else {
         const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
         const int pc = lane % kDChunksPerRow;
         const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
-        d_off[q] = (uint32_t)(k * p.d_ld + c * 16);
+        if constexpr (kGroupedSdd) {
+          const int jb = (c * 8) / kBlock;
+          d_off[q] = (uint32_t)(k * p.d_ld +
+                                (grp_col(jb) + (c * 8) % kBlock) * 2);
+          ok = jb < grp_count;
+        } else {
+          d_off[q] = (uint32_t)(k * p.d_ld + c * 16);
+          ok = j0 + c * 8 < p.j_limit;
+        }
         d_lk[q] = k;
-        ok = j0 + c * 8 < p.j_limit;
       }
       if (!ok) d_off[q] = kOOB;
     }
@@ -431,8 +465,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       krem = p.k_limit - (int)k0;
       s_base = kSKC ? p.s_data + (long long)srow * kBM * p.s_ld + k0 * 2
                     : p.s_data + k0 * p.s_ld + (long long)srow * kBM * 2;
-      d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + k0 * 2
-                    : p.d_data + k0 * p.d_ld + (long long)j0 * 2;
+      if constexpr (kGroupedSdd)  // columns live in the lane offsets
+        d_base = kDKC ? p.d_data + k0 * 2 : p.d_data + k0 * p.d_ld;
+      else
+        d_base = kDKC ? p.d_data + (long long)j0 * p.d_ld + k0 * 2
+                      : p.d_data + k0 * p.d_ld + (long long)j0 * 2;
     } else {
       const int e = step / kStepsPerBlock;
       const int h = step % kStepsPerBlock;
@@ -782,8 +819,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
             *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
         char *dst;
         if constexpr (kSparseOut) {
-          dst = p.c_data + out_block * (kBlock * kBlock * 2) +
-                row * (kBlock * 2) + cc * 16;
+          const int jcol = jp0 + cc * 8;  // column inside the tile
+          const int jb = jcol / kBlock;
+          if (jb >= grp_count) continue;
+          dst = p.c_data + (grp_b0 + jb) * (kBlock * kBlock * 2) +
+                row * (kBlock * 2) + (jcol % kBlock) * 2;
         } else if constexpr (kOutT) {
           const int jrow = j0 + jp0 + row;
           if (jrow >= p.j_limit) continue;
@@ -897,8 +937,90 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     // ==== one output tile per workgroup ===================================
     const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                        : xcd_tile(blockIdx.x, gridDim.x);
-    if constexpr (kSparseOut) {
+    if constexpr (kGroupedSdd) {
+      // Tile t = group t of the row-major list of groups, a block-row
+      // contributing ceil(n_r / kGrp) groups of consecutive stored blocks.
+      // One parallel scan of the group counts over C's offsets (each lane a
+      // contiguous run of rows; wave scan by shuffles, then wave totals); the
+      // grid is the host's upper bound nb/kGrp + R, so late tiles exit.
+      const int R = p.num_rows;
+      const int per = (R + kThreads - 1) / kThreads;
+      const int r0 = min(R, tid * per), r1 = min(R, r0 + per);
+      int local = 0;
+      for (int r = r0; r < r1; ++r)
+        local += (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
+      int incl = local;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+      }
+      // Row group counts' min / max: when every row has the same count G
+      // (block-rows sharing one column set, e.g. the MoE expert-diagonal),
+      // tiles run group-major (t -> group t / R, row t % R), so the
+      // workgroups that run together on an XCD share one D column slice in
+      // its L2 instead of each streaming a different one from HBM.
+      int gmin = 0x7fffffff, gmax = 0;
+      for (int r = r0; r < r1; ++r) {
+        const int g =
+            (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
+        gmin = min(gmin, g);
+        gmax = max(gmax, g);
+      }
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        gmin = min(gmin, __shfl_xor(gmin, d, 64));
+        gmax = max(gmax, __shfl_xor(gmax, d, 64));
+      }
+      int *wsum = reinterpret_cast<int *>(lds);
+      if (lane == 63) {
+        wsum[wave] = incl;
+        wsum[kNW + wave] = gmin;
+        wsum[2 * kNW + wave] = gmax;
+      }
+      __syncthreads();
+      int before = 0, total = 0;
+      for (int w2 = 0; w2 < kNW; ++w2) {
+        const int v = wsum[w2];
+        before += w2 < wave ? v : 0;
+        total += v;
+        gmin = min(gmin, wsum[kNW + w2]);
+        gmax = max(gmax, wsum[2 * kNW + w2]);
+      }
+      int start = before + incl - local;
+      const bool uniform = gmin == gmax;
+      if (!uniform) {
+        for (int r = r0; r < r1; ++r) {
+          const int g =
+              (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
+          if (tile >= start && tile < start + g) {
+            scratch[0] = r;
+            scratch[1] = tile - start;
+          }
+          start += g;
+        }
+      }
+      __syncthreads();
+      if (tile >= total) return;  // whole workgroup: no barrier pending
+      int gi;
+      if (uniform) {
+        srow = tile % R;
+        gi = tile / R;
+      } else {
+        srow = __builtin_amdgcn_readfirstlane(scratch[0]);
+        gi = __builtin_amdgcn_readfirstlane(scratch[1]);
+      }
+      const int b0 = p.c_offsets[srow] + gi * kGrp;
+      grp_b0 = b0;
+      grp_count = min(kGrp, p.c_offsets[srow + 1] - b0);
+      grp_c0 = p.c_indices[b0] * kBlock;
+      if (kGrp > 1 && grp_count > 1) grp_c1 = p.c_indices[b0 + 1] * kBlock;
+      if (kGrp > 2 && grp_count > 2) grp_c2 = p.c_indices[b0 + 2] * kBlock;
+      if (kGrp > 3 && grp_count > 3) grp_c3 = p.c_indices[b0 + 3] * kBlock;
+      __syncthreads();  // wsum / scratch reads done before the ring is used
+    } else if constexpr (kSparseOut) {
       out_block = tile;
+      grp_b0 = tile;
       srow = p.c_row_indices[tile];
       j0 = p.c_indices[tile] * kBlock;
     } else {
@@ -945,8 +1067,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 }
 
 // Host-side launch of one instantiation (defined in block_gemm.hip).
+// grouped: SDD on CfgSddGrouped (params.num_tiles = the grid's upper bound).
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
-                           bool out_t, const GemmParams &params,
+                           bool out_t, bool grouped, const GemmParams &params,
                            hipStream_t stream);
 
 }  // namespace sputnik_amd

@@ -10,48 +10,61 @@
 namespace sputnik_amd {
 namespace {
 
-template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT>
-hipError_t Launch(const GemmParams &p, hipStream_t stream) {
-  if (p.num_tiles <= 0) return hipSuccess;
-  using Cfg = typename std::conditional<kSparseOut, CfgSdd, CfgSparse>::type;
+template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
+          class Cfg>
+hipError_t LaunchCfg(const GemmParams &p, hipStream_t stream) {
   hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, Cfg>),
                      dim3(p.num_tiles), dim3(64 * Cfg::kWM * Cfg::kWN), 0,
                      stream, p);
   return hipGetLastError();
 }
 
+template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT>
+hipError_t Launch(const GemmParams &p, bool grouped, hipStream_t stream) {
+  if (p.num_tiles <= 0) return hipSuccess;
+  if constexpr (kSparseOut) {
+    if (grouped)
+      return LaunchCfg<T, true, kSKC, kDKC, false, CfgSddGrouped>(p, stream);
+    return LaunchCfg<T, true, kSKC, kDKC, false, CfgSdd>(p, stream);
+  } else {
+    return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSparse>(p, stream);
+  }
+}
+
 template <typename T>
 hipError_t LaunchTyped(bool sparse_out, bool s_kc, bool d_kc, bool out_t,
-                       const GemmParams &p, hipStream_t stream) {
+                       bool g, const GemmParams &p, hipStream_t stream) {
   const int code = (s_kc ? 4 : 0) | (d_kc ? 2 : 0) | (out_t ? 1 : 0);
   if (sparse_out) {
     switch (code & 6) {
-      case 6: return Launch<T, true, true, true, false>(p, stream);   // SDD NT
-      case 4: return Launch<T, true, true, false, false>(p, stream);  // SDD NN
-      case 2: return Launch<T, true, false, true, false>(p, stream);  // SDD TT
-      default: return Launch<T, true, false, false, false>(p, stream);  // TN
+      case 6: return Launch<T, true, true, true, false>(p, g, stream);   // SDD NT
+      case 4: return Launch<T, true, true, false, false>(p, g, stream);  // SDD NN
+      case 2: return Launch<T, true, false, true, false>(p, g, stream);  // SDD TT
+      default: return Launch<T, true, false, false, false>(p, g, stream);  // TN
     }
   }
   switch (code) {
-    case 4: return Launch<T, false, true, false, false>(p, stream);  // DSD NN
-    case 6: return Launch<T, false, true, true, false>(p, stream);   // DSD NT
-    case 0: return Launch<T, false, false, false, false>(p, stream); // DSD TN
-    case 2: return Launch<T, false, false, true, false>(p, stream);  // DSD TT
-    case 3: return Launch<T, false, false, true, true>(p, stream);   // DDS NN
-    case 7: return Launch<T, false, true, true, true>(p, stream);    // DDS NT
-    case 1: return Launch<T, false, false, false, true>(p, stream);  // DDS TN
-    default: return Launch<T, false, true, false, true>(p, stream);  // DDS TT
+    case 4: return Launch<T, false, true, false, false>(p, g, stream);  // DSD NN
+    case 6: return Launch<T, false, true, true, false>(p, g, stream);   // DSD NT
+    case 0: return Launch<T, false, false, false, false>(p, g, stream); // DSD TN
+    case 2: return Launch<T, false, false, true, false>(p, g, stream);  // DSD TT
+    case 3: return Launch<T, false, false, true, true>(p, g, stream);   // DDS NN
+    case 7: return Launch<T, false, true, true, true>(p, g, stream);    // DDS NT
+    case 1: return Launch<T, false, false, false, true>(p, g, stream);  // DDS TN
+    default: return Launch<T, false, true, false, true>(p, g, stream);  // DDS TT
   }
 }
 
 }  // namespace
 
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
-                           bool out_t, const GemmParams &params,
+                           bool out_t, bool grouped, const GemmParams &params,
                            hipStream_t stream) {
   if (dtype == 1)
-    return LaunchTyped<__bf16>(sparse_out, s_kc, d_kc, out_t, params, stream);
-  return LaunchTyped<_Float16>(sparse_out, s_kc, d_kc, out_t, params, stream);
+    return LaunchTyped<__bf16>(sparse_out, s_kc, d_kc, out_t, grouped, params,
+                               stream);
+  return LaunchTyped<_Float16>(sparse_out, s_kc, d_kc, out_t, grouped, params,
+                               stream);
 }
 
 }  // namespace sputnik_amd

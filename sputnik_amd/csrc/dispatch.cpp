@@ -289,6 +289,39 @@ int AsCode(Status st) {
   }
 }
 
+// Grouped SDD tiles (CfgSddGrouped: up to 4 stored blocks of a block-row per
+// workgroup) when there are enough groups to fill the CUs, the rows fit the
+// in-kernel group scan, and every gathered D offset fits the 31-bit lane
+// offset. Sets the grid to the upper bound nb/4 + rows; surplus workgroups
+// exit at once.
+constexpr int kMaxGroupRows = 32767;
+bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
+#ifdef SPUTNIK_NO_GROUPED_SDD
+  return false;
+#endif
+  static const int disabled = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_GROUPED_SDD");
+    return e != nullptr && std::atoi(e) == 0;
+  }();
+  if (disabled || c.offsets == nullptr) return false;
+  constexpr int kGrp = CfgSddGrouped::kBN / kBlock;
+  const int blocks = p->num_tiles;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                            dev) != hipSuccess)
+    return false;
+  if (blocks < kGrp * cus || p->num_rows > kMaxGroupRows) return false;
+  // D lane offsets: k-contiguous D gathers whole rows (n * ldb); otherwise
+  // one 32-row k panel plus any column.
+  const long long span = d_kc ? (long long)p->j_limit * p->d_ld
+                              : 32LL * p->d_ld + (long long)p->j_limit * 2;
+  if (span > kMaxLaneOffset) return false;
+  p->c_offsets = static_cast<const int *>(c.offsets);
+  p->num_tiles = blocks / kGrp + p->num_rows + 1;
+  return true;
+}
+
 }  // namespace
 
 // ---- shared entry points -------------------------------------------------
@@ -307,7 +340,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, stream);
-  return LaunchBlockGemm(dtype, false, !ta, tb, false, p, stream);
+  return LaunchBlockGemm(dtype, false, !ta, tb, false, false, p, stream);
 }
 
 hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
@@ -325,7 +358,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   p.debug = g_debug;
   PreparePairs(&p, stream);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
-                         /*out_t=*/true, p, stream);
+                         /*out_t=*/true, false, p, stream);
 }
 
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
@@ -336,8 +369,9 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
   p.debug = g_debug;
-  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false, p,
-                         stream);
+  const bool grouped = UseGroupedSdd(&p, c, tb);
+  return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
+                         grouped, p, stream);
 }
 
 }  // namespace sputnik_amd

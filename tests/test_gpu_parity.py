@@ -356,6 +356,22 @@ def test_sdd_ragged_k(k):
             H.assert_close(gpu, ref, "f16", f"sdd k={k} {ta}{tb}")
 
 
+@pytest.mark.parametrize("k", [200, 1024])
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_sdd_grouped_tiles(k, dtype):
+    """Enough output blocks (>= 4 per CU) for the grouped SDD tiles: up to 4
+    consecutive stored blocks of a block-row per workgroup, rows whose block
+    counts are not multiples of 4, unordered columns, a K tail, all four
+    transposes; every block against the oracle."""
+    m, n = 4096, 8192
+    for ta in (False, True):
+        for tb in (False, True):
+            p = dict(m=m, k=k, n=n, nonzeros=1201 * 16384, ta=ta, tb=tb,
+                     unordered=True)
+            gpu, ref = run_sdd(p, dtype=dtype, seed=k + 2 * ta + tb)
+            H.assert_close(gpu, ref, dtype, f"sdd-grouped {ta}{tb} k={k}")
+
+
 def test_sdd_dds_pair_config3():
     """BASELINE config 3 (MegaBlocks fwd/bwd pair at 4096^3, 20%), sampled."""
     rng = np.random.default_rng(11)
