@@ -601,6 +601,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr int kSlotBytes = kBM * kBN * 4;
   constexpr int kSc1 = 16;  // cache-policy bits: sc1
   int pair_id = 0;
+  int pair_target = 0;  // blocks per workgroup the pair schedule aims at
   auto pair_rsrc = [&]() {
     return make_rsrc(reinterpret_cast<const char *>(p.pair_partials));
   };
@@ -846,7 +847,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   auto rank_rows = [&](int ra, int rb) {
     const int R = p.num_rows;
     int *offs = reinterpret_cast<int *>(lds);
+    int *n_by_rank = offs + R + 1;
     for (int r = tid; r <= R; r += kThreads) offs[r] = p.s_offsets[r];
+    if (tid == 0) scratch[2] = 0;
     __syncthreads();
     for (int r = tid; r < R; r += kThreads) {
       const int nr = offs[r + 1] - offs[r];
@@ -855,12 +858,22 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
         const int n2 = offs[r2 + 1] - offs[r2];
         rank += (n2 > nr) | ((n2 == nr) & (r2 < r));
       }
+      n_by_rank[rank] = nr;
       if (rank == ra) scratch[0] = r;
       if (rank == rb) scratch[1] = r;
     }
     __syncthreads();
+    // Balanced target of the pair schedule: the largest pair mean (rank i
+    // with rank R-1-i, rounded up; the middle row of odd R alone).
+    for (int i = tid; i < (R + 1) / 2; i += kThreads) {
+      const int j = R - 1 - i;
+      const int v = i == j ? n_by_rank[i] : (n_by_rank[i] + n_by_rank[j] + 1) / 2;
+      atomicMax(&scratch[2], v);
+    }
+    __syncthreads();
     const int row_a = __builtin_amdgcn_readfirstlane(scratch[0]);
     const int row_b = __builtin_amdgcn_readfirstlane(scratch[1]);
+    pair_target = __builtin_amdgcn_readfirstlane(scratch[2]);
     __syncthreads();
     return make_int2(row_a, row_b);
   };
@@ -915,7 +928,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     const int n_h = p.s_offsets[rows.x + 1] - e_h;
     const int e_l = p.s_offsets[rows.y];
     const int n_l = p.s_offsets[rows.y + 1] - e_l;
-    const int hb = role == 1 ? 0 : (n_h - n_l) >> 1;
+    // Hand over only what exceeds the panel's balanced target, and nothing
+    // under kMinHandoff blocks: a hand-off costs each side about one
+    // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
+    constexpr int kMinHandoff = 2;
+    int hb = role == 1 ? 0 : n_h - pair_target;
+    if (hb < kMinHandoff) hb = 0;
     pair_id = panel * half + pi;
     j0 = panel * kBN;
     if (role == 0) {
