@@ -417,7 +417,7 @@ def main():
         "unit": "TFLOP/s",
         "frac": round(achieved / PEAK_MFMA_TFLOPS, 4),
         "traffic": traffic,
-        "kernel": "block_gemm_kernel<f16, DSD NN, BN=256>",
+        "kernel": "block_gemm_kernel<f16, DSD NN, CfgWide8S: 128x512 tile, staggered>",
         "algorithmic_bytes": prob.bytes,
         "algorithmic_flops": prob.flops,
     }

@@ -767,6 +767,31 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // ---- output of one finished tile: fp32 -> T, staged through LDS, 16-byte
   // coalesced stores. The tile is staged in kPasses slices of kPassJ dense
   // columns (j) when it does not fit in the ring at once (128 x 512 tiles).
+  // A dense-output tile of an empty block-row is all zeros: store them
+  // straight from registers (no LDS staging, no barrier), 16 B per lane.
+  auto write_zero_tile = [&]() {
+    constexpr int kRows = kOutT ? kBN : kBM;   // rows of the output image
+    constexpr int kCols = kOutT ? kBM : kBN;
+    constexpr int kChunksPerRow = kCols / 8;
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (int id = tid; id < kRows * kChunksPerRow; id += kThreads) {
+      const int row = id / kChunksPerRow;
+      const int cc = id % kChunksPerRow;
+      char *dst;
+      if constexpr (kOutT) {
+        const int jrow = j0 + row;
+        if (jrow >= p.j_limit) continue;
+        dst = p.c_data + (long long)jrow * p.c_ld +
+              ((long long)srow * kBM + cc * 8) * 2;
+      } else {
+        const int jcol = j0 + cc * 8;
+        if (jcol >= p.j_limit) continue;
+        dst = p.c_data + ((long long)srow * kBM + row) * p.c_ld +
+              (long long)jcol * 2;
+      }
+      *reinterpret_cast<uint4 *>(dst) = z;
+    }
+  };
   auto write_tile = [&](long long out_block) {
     wait_vmcnt<0>();
     __syncthreads();
@@ -1080,7 +1105,13 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     run_sparse(entry0, 0, entries * kStepsPerBlock);
   }
   exp_stamp(p.debug, 3, __builtin_amdgcn_s_memrealtime());
-  write_tile(out_block);
+  bool empty = false;
+  if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
+  if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
+  if (empty)
+    write_zero_tile();
+  else
+    write_tile(out_block);
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
 }
 
