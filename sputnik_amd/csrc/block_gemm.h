@@ -205,12 +205,16 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
 }
 
 // Experiment builds: record (wave 0, lane 0) a per-workgroup timeline.
-// Layout per workgroup: [realtime start, memtime start, memtime prologue end,
-// realtime loop end, memtime end, xcc_id, hw_id, k-steps].
+// Layout per workgroup (16 slots): [realtime start, memtime start, memtime
+// prologue end, realtime loop end, memtime end (stores drained), xcc_id,
+// hw_id, k-steps, memtime after the pipeline fill, memtime after the pair
+// publish, memtime after the pipeline, memtime after the pair collect, role
+// (0 light, 1 middle, 2 heavy, 3 unpaired), memtime before the tile stores,
+// realtime end].
 __device__ __forceinline__ void exp_stamp(unsigned long long *dbg, int slot,
                                           unsigned long long v) {
   if constexpr ((SPUTNIK_EXP & 16) != 0) {
-    if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 8 + slot] = v;
+    if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + slot] = v;
   }
 }
 
@@ -572,7 +576,16 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       for (int a = 0; a < kFM; ++a)
 #pragma unroll
         for (int b = 0; b < kFN; ++b)
-          acc[a][b] = MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b], acc[a][b]);
+          // Straight outputs compute the tile transposed (D fragment as
+          // the MFMA's A operand), so a lane's 4 accumulator values are 4
+          // consecutive output columns of one row: the epilogue then packs
+          // them into one 8-byte LDS write. Transposed outputs (DDS) keep
+          // S as the A operand: 4 consecutive rows = 4 consecutive
+          // elements of an output row of C.
+          acc[a][b] = kOutT ? MfmaTraits<T>::mfma(F.a[kk][a], F.b[kk][b],
+                                                  acc[a][b])
+                            : MfmaTraits<T>::mfma(F.b[kk][b], F.a[kk][a],
+                                                  acc[a][b]);
 #if SPUTNIK_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -677,6 +690,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     Frags f0, f1;
     read_step(0, f0);
     wait_step(f0);
+    exp_stamp(p.debug, 8, __builtin_amdgcn_s_memtime());
     // Staggered configs: the lagging half (waves kNW/2..) passes one barrier
     // behind the leading half, and every step has two barriers, B1 before
     // the DMA/read phase and B2 before the MFMA phase, so a lagging wave's
@@ -730,7 +744,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       mfma_step(cur);
       if (i + 1 < steps) wait_step(next);
       if constexpr (kPairs) {
-        if (i + 1 == flush_at) publish();
+        if (i + 1 == flush_at) {
+          publish();
+          exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
+        }
       }
       slot = nslot;
     };
@@ -817,25 +834,27 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
         for (int b = 0; b < kFN; ++b) {
           const int jb = col_w + 16 * b;  // wave-uniform
           if (jb < jp0 || jb >= jp0 + kPassJ) continue;
-          const int i = row_w + 16 * a + 4 * (lane >> 4);
-          const int j = jb - jp0 + (lane & 15);
+          typedef T t4 __attribute__((ext_vector_type(4)));
+          t4 v;
+          v[0] = (T)acc[a][b][0];
+          v[1] = (T)acc[a][b][1];
+          v[2] = (T)acc[a][b][2];
+          v[3] = (T)acc[a][b][3];
           if constexpr (kOutT) {
-            typedef T t4 __attribute__((ext_vector_type(4)));
-            t4 v;
-            v[0] = (T)acc[a][b][0];
-            v[1] = (T)acc[a][b][1];
-            v[2] = (T)acc[a][b][2];
-            v[3] = (T)acc[a][b][3];
+            // lane: rows i..i+3 of column j -> staging row j
+            const int i = row_w + 16 * a + 4 * (lane >> 4);
+            const int j = jb - jp0 + (lane & 15);
             *reinterpret_cast<t4 *>(st + j * kStLd + i * 2) = v;
           } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              *reinterpret_cast<T *>(st + (i + r) * kStLd + j * 2) =
-                  (T)acc[a][b][r];
+            // lane: columns j..j+3 of row i (the MFMA computed O^T)
+            const int i = row_w + 16 * a + (lane & 15);
+            const int j = jb - jp0 + 4 * (lane >> 4);
+            *reinterpret_cast<t4 *>(st + i * kStLd + j * 2) = v;
           }
         }
       }
       __syncthreads();
+      if (pass == 0) exp_stamp(p.debug, 13, __builtin_amdgcn_s_memtime());
       constexpr int kChunksPerRow = kOutCols / 8;
       constexpr int kChunks = kOutRows * kChunksPerRow;
       for (int id = tid; id < kChunks; id += kThreads) {
@@ -876,6 +895,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     for (int r = tid; r <= R; r += kThreads) offs[r] = p.s_offsets[r];
     if (tid == 0) scratch[2] = 0;
     __syncthreads();
+    exp_stamp(p.debug, 15, __builtin_amdgcn_s_memtime());
     for (int r = tid; r < R; r += kThreads) {
       const int nr = offs[r + 1] - offs[r];
       int rank = 0;
@@ -899,7 +919,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     const int row_a = __builtin_amdgcn_readfirstlane(scratch[0]);
     const int row_b = __builtin_amdgcn_readfirstlane(scratch[1]);
     pair_target = __builtin_amdgcn_readfirstlane(scratch[2]);
-    __syncthreads();
+    // No closing barrier: the caller reads the staged offsets and then
+    // synchronizes before the ring (which overlaps them) is written.
     return make_int2(row_a, row_b);
   };
 
@@ -949,10 +970,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       pi = t % half;
     }
     const int2 rows = rank_rows(pi, R - 1 - pi);
-    const int e_h = p.s_offsets[rows.x];
-    const int n_h = p.s_offsets[rows.x + 1] - e_h;
-    const int e_l = p.s_offsets[rows.y];
-    const int n_l = p.s_offsets[rows.y + 1] - e_l;
+    // The offsets are still staged in LDS by rank_rows (the ring is not
+    // written before the first DMA): no dependent global round trip.
+    const int *offs = reinterpret_cast<const int *>(lds);
+    const int e_h = __builtin_amdgcn_readfirstlane(offs[rows.x]);
+    const int n_h = __builtin_amdgcn_readfirstlane(offs[rows.x + 1]) - e_h;
+    const int e_l = __builtin_amdgcn_readfirstlane(offs[rows.y]);
+    const int n_l = __builtin_amdgcn_readfirstlane(offs[rows.y + 1]) - e_l;
+    __syncthreads();  // staged offsets / scratch read by every wave
     // Hand over only what exceeds the panel's balanced target, and nothing
     // under kMinHandoff blocks: a hand-off costs each side about one
     // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
@@ -961,6 +986,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     if (hb < kMinHandoff) hb = 0;
     pair_id = panel * half + pi;
     j0 = panel * kBN;
+    exp_stamp(p.debug, 12, role);
     if (role == 0) {
       srow = rows.y;
       idx_base = e_h;
@@ -978,6 +1004,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     }
   } else {
     // ==== one output tile per workgroup ===================================
+    exp_stamp(p.debug, 12, 3);
     const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                        : xcd_tile(blockIdx.x, gridDim.x);
     if constexpr (kGroupedSdd) {
@@ -1079,10 +1106,16 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
       j0 = panel * kBN;
       srow = target;
-      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows)
+      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
         srow = rank_rows(target, target).x;
-      entry0 = p.s_offsets[srow];
-      entries = p.s_offsets[srow + 1] - entry0;
+        const int *offs = reinterpret_cast<const int *>(lds);  // staged
+        entry0 = __builtin_amdgcn_readfirstlane(offs[srow]);
+        entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
+        __syncthreads();  // staged offsets / scratch read by every wave
+      } else {
+        entry0 = p.s_offsets[srow];
+        entries = p.s_offsets[srow + 1] - entry0;
+      }
       idx_base = entry0;
       p_first = 0;
       p_steps = entries * kStepsPerBlock;
@@ -1099,7 +1132,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     exp_stamp(p.debug, 7, p_steps);
     cached_e = -1;
     pipeline(p_first, p_steps, p_flush);
+    exp_stamp(p.debug, 10, __builtin_amdgcn_s_memtime());
     if (do_collect) collect();
+    exp_stamp(p.debug, 11, __builtin_amdgcn_s_memtime());
   } else {
     exp_stamp(p.debug, 7, entries * kStepsPerBlock);
     run_sparse(entry0, 0, entries * kStepsPerBlock);
@@ -1112,7 +1147,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     write_zero_tile();
   else
     write_tile(out_block);
+  if constexpr ((SPUTNIK_EXP & 16) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
+  exp_stamp(p.debug, 14, __builtin_amdgcn_s_memrealtime());
 }
 
 // Host-side launch of one instantiation (defined in block_gemm.hip).
