@@ -11,10 +11,10 @@ step() { local name=$1 to=$2; shift 2; echo "== $name" | tee -a $OUT/steps.log
   echo "== $name rc=$rc" | tee -a $OUT/steps.log; tail -3 $OUT/$name.log; return $rc; }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; fatal $rc && exit $rc
-step pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider; rc=$?; fatal $rc && exit $rc
+step pytest_gpu 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread; rc=$?; fatal $rc && exit $rc
 R=$GRAFT_REPO_ROOT
 ( cd /tmp && for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
-    i=$((${i:-0}+1)); timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -f csv -d $R/$OUT/pmc/p$i -o pass -- \
+    i=$((${i:-0}+1)); timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -f csv -d $R/$OUT/pmc/p$i -o pass -- \
       python3 $R/bench.py --steps 20 --warmup 3 --sweep "" --no-cpu > $R/$OUT/pmc_p$i.log 2>&1 || exit $?
   done ); rc=$?; echo "== pmc rc=$rc" | tee -a $OUT/steps.log; fatal $rc && exit $rc
 python scripts/pmc_traffic.py $OUT/pmc dsd_4096x4096x4096_0.5_f16 $OUT/pmc_latest.json

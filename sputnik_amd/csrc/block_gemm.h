@@ -51,6 +51,26 @@
 #ifndef SPUTNIK_EXP
 #define SPUTNIK_EXP 0
 #endif
+// Cache-policy bits (buffer aux: 1 sc0, 2 nt, 16 sc1) of the sparse-operand
+// and dense-operand DMA. On an XCD every sparse block is read once (the XCD
+// owns one dense panel), so it is streamed with nt by default and leaves the
+// L2 to the dense panel that every workgroup of the XCD re-reads.
+#ifndef SPUTNIK_S_AUX
+#define SPUTNIK_S_AUX 0
+#endif
+#ifndef SPUTNIK_D_AUX
+#define SPUTNIK_D_AUX 0
+#endif
+// Scalar-index configs: load the next stored block's (k-block, storage
+// block) one block ahead, so the scalar-cache round trip is off the DMA
+// issue path.
+#ifndef SPUTNIK_IDX_PREFETCH
+#define SPUTNIK_IDX_PREFETCH 0
+#endif
+// Staggered configs: static s_setprio(1) for the lagging (younger) half.
+#ifndef SPUTNIK_LAG_PRIO
+#define SPUTNIK_LAG_PRIO 0
+#endif
 
 namespace sputnik_amd {
 
@@ -157,10 +177,11 @@ __device__ __forceinline__ int scalar_load_int(const int *base, int e) {
   return *(const __attribute__((address_space(4))) int *)(base + e);
 }
 
+template <int kAux = 0>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds_dst,
                                       uint32_t voffset) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, SPUTNIK_LDS(lds_dst), 16,
-                                           voffset, 0, 0, 0);
+                                           voffset, 0, 0, kAux);
 }
 
 // 16x32 operand fragment from a k-contiguous image [rows][BK] (kRowBytes =
@@ -456,6 +477,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // idx_split entries (a pair producer's second segment), idx_base2 + e -
   // idx_split.
   int idx_base = 0, idx_split = 0x7fffffff, idx_base2 = 0;
+  // Index prefetch (SPUTNIK_IDX_PREFETCH): entry pf_e's values, and the end
+  // of the pipeline's entry range (no load past it).
+  int pf_e = -1, pf_kblk = 0, pf_blk = 0, e_end = 0;
   const char *blk_s = nullptr;
   const char *blk_d = nullptr;
   auto issue = [&](int step, int slot) {
@@ -478,16 +502,43 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       const int e = step / kStepsPerBlock;
       const int h = step % kStepsPerBlock;
       if (e != cached_e) {
-        cached_e = e;
         int kblk, blk;
         if constexpr (kScalarIdx) {
-          const int ge =
-              e < idx_split ? idx_base + e : idx_base2 + (e - idx_split);
-          kblk = scalar_load_short(p.s_indices, ge);
-          blk = p.s_block_offsets != nullptr
-                    ? scalar_load_int(p.s_block_offsets, ge)
-                    : ge;
+          auto entry = [&](int x) {
+            return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
+          };
+          if constexpr (SPUTNIK_IDX_PREFETCH != 0) {
+            // pf_kblk / pf_blk hold entry cached_e + 1 when it was
+            // prefetched (pf_e == e); the next entry is loaded now, while
+            // this block's 4 steps run.
+            if (pf_e == e) {
+              kblk = pf_kblk;
+              blk = pf_blk;
+            } else {
+              const int ge = entry(e);
+              kblk = scalar_load_short(p.s_indices, ge);
+              blk = p.s_block_offsets != nullptr
+                        ? scalar_load_int(p.s_block_offsets, ge)
+                        : ge;
+            }
+            if (e + 1 < e_end) {
+              const int gn = entry(e + 1);
+              pf_kblk = scalar_load_short(p.s_indices, gn);
+              pf_blk = p.s_block_offsets != nullptr
+                           ? scalar_load_int(p.s_block_offsets, gn)
+                           : gn;
+              pf_e = e + 1;
+            }
+          } else {
+            const int ge = entry(e);
+            kblk = scalar_load_short(p.s_indices, ge);
+            blk = p.s_block_offsets != nullptr
+                      ? scalar_load_int(p.s_block_offsets, ge)
+                      : ge;
+          }
+          cached_e = e;
         } else {
+          cached_e = e;
           kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
           blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
         }
@@ -507,13 +558,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     for (int q = 0; q < kSInstr; ++q) {
       uint32_t off = s_off[q];
       if constexpr (kSparseOut) off = s_lk[q] < krem ? off : kOOB;
-      dma16(rs, slot_base + (wave * kSInstr + q) * 1024, off);
+      dma16<kSparseOut ? 0 : SPUTNIK_S_AUX>(
+          rs, slot_base + (wave * kSInstr + q) * 1024, off);
     }
 #pragma unroll
     for (int q = 0; q < kDInstr; ++q) {
       uint32_t off = d_off[q];
       if constexpr (kSparseOut) off = d_lk[q] < krem ? off : kOOB;
-      dma16(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024, off);
+      dma16<SPUTNIK_D_AUX>(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024,
+                           off);
     }
   };
 
@@ -677,6 +730,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // streaming.
   auto pipeline = [&](int first, int steps, int flush_at = -1) {
     if (steps <= 0) return;
+    e_end = (first + steps + kStepsPerBlock - 1) / kStepsPerBlock;
+    pf_e = -1;
     issue(first, 0);
     if (steps > 1) issue(first + 1, 1);
     if (steps > 2) issue(first + 2, 2);
@@ -706,6 +761,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     // Every wave executes the same number of barriers: laggers add one after
     // the prologue, leaders one after the loop.
     const bool lag = Cfg::kStagger && wave >= kNW / 2;
+    if constexpr (SPUTNIK_LAG_PRIO != 0) {
+      if (lag) __builtin_amdgcn_s_setprio(1);
+    }
     if (lag) {
       if (steps > 2)
         wait_vmcnt<kGroup>();
