@@ -40,7 +40,9 @@ def main():
     for _ in range(30):
         assert fn(ctypes.byref(ca), 0, ctypes.byref(cb), 0, ctypes.byref(cc), 0, stream) == 0
     torch.cuda.synchronize()
-    d = dbg.cpu().numpy().reshape(tiles, 16).astype(np.int64)
+    d = dbg.cpu().numpy().reshape(tiles, 16).astype(np.int64)[:2048]
+    g_all = int((d[:, 4] != 0).sum())
+    steps_all = d[:g_all, 7]
     d = d[d[:, 4] != 0]
     if args.dump:
         np.save(args.dump, d)
@@ -75,6 +77,16 @@ def main():
             r["head_publish"] = [int(np.median(hd)), int(hd.max())]
         r["end_us"] = [round(float(np.percentile((d[m, 14] - t0) / 100, q)), 2) for q in (0, 50, 100)]
         out[name] = r
+    # SPUTNIK_EXP & 128 builds: per-segment k-loop cycle sums of waves 0
+    # (leading half) and kNW/2 (lagging half), per step.
+    raw = dbg.cpu().numpy().astype(np.int64)
+    seg = raw[2048 * 16:2048 * 16 + g_all * 16].reshape(g_all, 16) if g_all else None
+    if seg is not None and seg.any():
+        names = ["vmcnt+B1", "dma_issue", "read_issue", "lagwait+B2", "mfma_issue", "read_wait"]
+        st = np.maximum(steps_all, 1)[:, None]
+        for half, off in (("lead", 0), ("lag", 8)):
+            per = seg[:, off:off + 6] / st
+            out["seg_" + half] = {n: round(float(np.median(per[:, q])), 1) for q, n in enumerate(names)}
     print(json.dumps(out))
 
 

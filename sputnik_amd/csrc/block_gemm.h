@@ -67,9 +67,13 @@
 #ifndef SPUTNIK_IDX_PREFETCH
 #define SPUTNIK_IDX_PREFETCH 0
 #endif
+// Fragment reads of the next step before this step's DMA issue.
+#ifndef SPUTNIK_READ_FIRST
+#define SPUTNIK_READ_FIRST 0
+#endif
 // Staggered configs: static s_setprio(1) for the lagging (younger) half.
 #ifndef SPUTNIK_LAG_PRIO
-#define SPUTNIK_LAG_PRIO 0
+#define SPUTNIK_LAG_PRIO 1
 #endif
 
 namespace sputnik_amd {
@@ -300,6 +304,11 @@ using CfgBlock2 = TileConfig<128, 2, 2, 32, 3, 2>;
 #define SPUTNIK_SPARSE_CFG CfgWide8S
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
+// DSD / DDS over tall sparse operands (more block-rows than kLptRows).
+#ifndef SPUTNIK_TALL_CFG
+#define SPUTNIK_TALL_CFG CfgDual
+#endif
+using CfgTall = SPUTNIK_TALL_CFG;
 #ifndef SPUTNIK_SDD_CFG
 #define SPUTNIK_SDD_CFG CfgBlock
 #endif
@@ -482,12 +491,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   int pf_e = -1, pf_kblk = 0, pf_blk = 0, e_end = 0;
   const char *blk_s = nullptr;
   const char *blk_d = nullptr;
-  auto issue = [&](int step, int slot) {
+  // issue() = prep() (scalar work: index lookup, tile bases) + fire() (the
+  // LDS-DMA instructions), so a step can put its fragment reads between them.
+  const char *s_base = nullptr;
+  const char *d_base = nullptr;
+  int krem = kBK;  // valid k in the prepared step (SDD tail)
+  auto prep = [&](int step) {
     if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
-    const char *s_base;
-    const char *d_base;
-    int krem = kBK;  // valid k in this step (SDD tail)
     if constexpr (kSparseOut) {
       const long long k0 = (long long)step * kBK;
       krem = p.k_limit - (int)k0;
@@ -551,6 +562,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       d_base = blk_d + (kDKC ? (long long)h * (kBK * 2)
                              : (long long)h * kBK * p.d_ld);
     }
+  };
+  auto fire = [&](int slot) {
+    if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     char *slot_base = lds + slot * kStageBytes;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(s_base);
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(d_base);
@@ -568,6 +582,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       dma16<SPUTNIK_D_AUX>(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024,
                            off);
     }
+  };
+  auto issue = [&](int step, int slot) {
+    prep(step);
+    fire(slot);
   };
 
   // Fragment registers of one k-step: [kk][f] for the S (a) and D (b)
@@ -728,6 +746,26 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // flush_at > 0: after the MFMAs of step flush_at - 1 the accumulators are
   // published (pair producer) and restarted from zero; the ring keeps
   // streaming.
+  // SPUTNIK_EXP & 128: per-segment cycle sums of the k-loop (waves 0 and
+  // kNW/2), read after wait_step so no stamp adds an LDS wait in the loop.
+  unsigned long long seg_t[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long seg_sum[6] = {0, 0, 0, 0, 0, 0};
+#define SEG_STAMP(n)                                          \
+  do {                                                        \
+    if constexpr ((SPUTNIK_EXP & 128) != 0) {                 \
+      __builtin_amdgcn_sched_barrier(0);                      \
+      seg_t[n] = __builtin_amdgcn_s_memtime();                \
+      __builtin_amdgcn_sched_barrier(0);                      \
+    }                                                         \
+  } while (0)
+#define SEG_ACCUM()                                           \
+  do {                                                        \
+    if constexpr ((SPUTNIK_EXP & 128) != 0) {                 \
+      _Pragma("unroll") for (int q = 0; q < 6; ++q)           \
+        seg_sum[q] += (seg_t[q] != 0 && seg_t[q + 1] > seg_t[q]) ? seg_t[q + 1] - seg_t[q] : 0; \
+      seg_t[1] = seg_t[2] = seg_t[3] = 0;                     \
+    }                                                         \
+  } while (0)
   auto pipeline = [&](int first, int steps, int flush_at = -1) {
     if (steps <= 0) return;
     e_end = (first + steps + kStepsPerBlock - 1) / kStepsPerBlock;
@@ -774,6 +812,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     int slot = 0;  // slot of step i
     auto body = [&](int i, Frags &cur, Frags &next) {
       const int nslot = slot + 1 == kStages ? 0 : slot + 1;
+      SEG_STAMP(0);
       if (i + 1 < steps) {
         if (!lag) {
           if (i + 2 < steps)
@@ -782,12 +821,34 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
             wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
-        if (i + 3 < steps) {
-          int dslot = slot + 3;
-          if (dslot >= kStages) dslot -= kStages;
-          issue(first + i + 3, dslot);
+        SEG_STAMP(1);
+        int dslot = slot + 3;
+        if (dslot >= kStages) dslot -= kStages;
+        if constexpr (SPUTNIK_READ_FIRST != 0) {
+          // Scalar prep first (its scalar-cache wait then finds no LDS read
+          // in flight). READ_FIRST 1: every wave reads, then fires its DMA.
+          // READ_FIRST 2/3: waves alternate the two orders (by wave bit 0 /
+          // bit 1), so while half of the memory-phase waves queue their DMA
+          // at the TA the other half's reads are served by the LDS.
+          if (i + 3 < steps) prep(first + i + 3);
+          const bool rf = SPUTNIK_READ_FIRST == 1 ||
+                          (SPUTNIK_READ_FIRST == 2 && (wave & 1) != 0) ||
+                          (SPUTNIK_READ_FIRST == 3 && (wave & 2) != 0);
+          if (rf) {
+            read_step(nslot, next);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i + 3 < steps) fire(dslot);
+          } else {
+            if (i + 3 < steps) fire(dslot);
+            __builtin_amdgcn_sched_barrier(0);
+            read_step(nslot, next);
+          }
+        } else {
+          if (i + 3 < steps) issue(first + i + 3, dslot);
+          SEG_STAMP(2);
+          read_step(nslot, next);
         }
-        read_step(nslot, next);
+        SEG_STAMP(3);
       }
       if constexpr (Cfg::kStagger) {
         if (lag) {
@@ -799,8 +860,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
         }
         __builtin_amdgcn_s_barrier();
       }
+      SEG_STAMP(4);
       mfma_step(cur);
+      SEG_STAMP(5);
       if (i + 1 < steps) wait_step(next);
+      SEG_STAMP(6);
+      SEG_ACCUM();
       if constexpr (kPairs) {
         if (i + 1 == flush_at) {
           publish();
@@ -1211,10 +1276,21 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   }
   exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
   exp_stamp(p.debug, 14, __builtin_amdgcn_s_memrealtime());
+  if constexpr ((SPUTNIK_EXP & 128) != 0) {
+    if (p.debug != nullptr && lane == 0 && (wave == 0 || wave == kNW / 2)) {
+      unsigned long long *o =
+          p.debug + 2048 * 16 + blockIdx.x * 16 + (wave == 0 ? 0 : 8);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) o[q] = seg_sum[q];
+    }
+  }
+#undef SEG_STAMP
+#undef SEG_ACCUM
 }
 
 // Host-side launch of one instantiation (defined in block_gemm.hip).
-// grouped: SDD on CfgSddGrouped (params.num_tiles = the grid's upper bound).
+// grouped: SDD on CfgSddGrouped (params.num_tiles = the grid's upper bound);
+// DSD / DDS on CfgTall (params.num_jtiles over CfgTall::kBN).
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
                            bool out_t, bool grouped, const GemmParams &params,
                            hipStream_t stream);

@@ -27,6 +27,11 @@ hipError_t Launch(const GemmParams &p, bool grouped, hipStream_t stream) {
       return LaunchCfg<T, true, kSKC, kDKC, false, CfgSddGrouped>(p, stream);
     return LaunchCfg<T, true, kSKC, kDKC, false, CfgSdd>(p, stream);
   } else {
+    // Tall sparse operands (many more tiles than CUs, no pair balancing):
+    // two 128x256 workgroups per CU, so one tile's prologue and epilogue
+    // overlap the other's pipeline.
+    if (grouped)
+      return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgTall>(p, stream);
     return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSparse>(p, stream);
   }
 }

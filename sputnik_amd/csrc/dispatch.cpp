@@ -166,7 +166,7 @@ Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   const MatmulShape s(a, ta, b, tb);
   if (!Aligned8(s)) return Status::kNoKernel;
   const bool d_kc = tb;  // B^T stored [N][K]: k-contiguous
-  if (!StrideOk(d_kc ? 256 : 64, s.ldb)) return Status::kNoKernel;
+  if (!StrideOk(d_kc ? CfgSparse::kBN : 64, s.ldb)) return Status::kNoKernel;
   *needs_meta = ta;
   if (ta && (a.offsets_t == nullptr || a.indices_t == nullptr ||
              a.block_offsets == nullptr))
@@ -197,7 +197,7 @@ Status PrepareDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   const MatmulShape s(a, ta, b, tb);
   if (!Aligned8(s)) return Status::kNoKernel;
   const bool d_kc = !ta;  // op(A)^T rows are A's rows when A is [M][K]
-  if (!StrideOk(d_kc ? 256 : 64, s.lda)) return Status::kNoKernel;
+  if (!StrideOk(d_kc ? CfgSparse::kBN : 64, s.lda)) return Status::kNoKernel;
   // Row n of op(B)^T is column n of B when B is stored [K][N] (tb == false).
   const bool col_order = !tb;
   *needs_meta = col_order;
@@ -322,6 +322,20 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   return true;
 }
 
+// Tall sparse operands (more block-rows than the in-kernel row ranking
+// handles, so no LPT order and no pair balancing) have many more tiles than
+// CUs: they run on CfgTall, two workgroups per CU.
+bool UseTall(GemmParams *p) {
+  static const int disabled = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_TALL");
+    return e != nullptr && std::atoi(e) == 0;
+  }();
+  if (disabled || p->num_rows <= kLptRows || p->pair != 0) return false;
+  p->num_jtiles = (p->j_limit + CfgTall::kBN - 1) / CfgTall::kBN;
+  p->num_tiles = p->num_rows * p->num_jtiles;
+  return true;
+}
+
 }  // namespace
 
 // ---- shared entry points -------------------------------------------------
@@ -340,7 +354,8 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, stream);
-  return LaunchBlockGemm(dtype, false, !ta, tb, false, false, p, stream);
+  const bool tall = UseTall(&p);
+  return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 
 hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
@@ -357,8 +372,9 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, stream);
+  const bool tall = UseTall(&p);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
-                         /*out_t=*/true, false, p, stream);
+                         /*out_t=*/true, tall, p, stream);
 }
 
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,

@@ -490,6 +490,30 @@ def test_tall_panel_config5_sampled():
         _sync()
         assert torch.equal(cp_t, c_t[r0 * 128:r1 * 128])
 
+@pytest.mark.parametrize("op", ["dsd", "dds"])
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_tall_sparse_operand(op, ta, tb, dtype):
+    """Sparse operands with more than 256 block-rows run on the tall tile
+    configuration (two 128x256 workgroups per CU, dispatch.cpp UseTall):
+    every transpose of DSD and DDS, a ragged dense extent (264: a partial
+    256-wide tile), unordered indices, both dtypes, full-output oracle."""
+    if dtype == "bf16" and (ta or tb):
+        pytest.skip("bf16 covered on NN")
+    tall = 300 * 128
+    nz = 240 * 16384
+    if op == "dsd":
+        p = dict(m=tall, k=256, n=264, nonzeros=nz, ta=ta, tb=tb,
+                 unordered=True)
+        gpu, ref, _, _ = run_dsd(p, dtype=dtype)
+    else:
+        p = dict(m=264, k=256, n=tall, nonzeros=nz, ta=ta, tb=tb,
+                 unordered=True)
+        gpu, ref = run_dds(p, dtype=dtype)
+    H.assert_close(gpu, ref, dtype, f"tall {op}")
+
+
 # ------------------------------------------------------------ metadata ----
 
 def _device_topology(offsets, indices, rows_b, cols_b):
