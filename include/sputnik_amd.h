@@ -85,6 +85,23 @@ int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
 /* reference sputnik/block/transpose/transpose.h:10 (device, bit-identical) */
 int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream);
 
+/* ---- Device topology builders (no host round trip) */
+/* Block mask (uint8 [block_rows][block_cols] row-major, nonzero = present)
+ * -> BCSR offsets int32[block_rows+1] and ascending int16 indices, the
+ * reference's mask -> CSR scan (sputnik/matrix_utils.cu:254-289, pad_rows_to
+ * = 1). `indices` must hold the mask's nonzero count (block_rows*block_cols
+ * bounds it); block_cols <= 32768. */
+int sputnik_mask_to_bcsr(const uint8_t *mask, int block_rows, int block_cols,
+                         int32_t *offsets, int16_t *indices, void *stream);
+/* MegaBlocks dMoE topology: padded_bins int32[num_experts] = cumulative
+ * per-expert token counts, each padded to a multiple of 128. Block-row r
+ * belongs to expert e = #{e : padded_bins[e] <= 128 r} (clamped to the last
+ * expert) and holds block-columns [e*blocks_per_expert, (e+1)*...).
+ * offsets int32[block_rows+1], indices int16[block_rows*blocks_per_expert]. */
+int sputnik_expert_topology(const int32_t *padded_bins, int num_experts,
+                            int block_rows, int blocks_per_expert,
+                            int32_t *offsets, int16_t *indices, void *stream);
+
 /* ---- Host-only queries (no GPU work; safe without a device) */
 /* 1 when the reference would accept the problem (same rules as
  * can_launch_* + ValidMatmul), 0 otherwise. op: 0=DSD 1=DDS 2=SDD. */

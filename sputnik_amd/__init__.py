@@ -95,6 +95,9 @@ _SIGNATURES = {
     "sputnik_sdd": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_row_indices": [_P, _P, _P],
     "sputnik_transpose": [_P, _P],
+    "sputnik_mask_to_bcsr": [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P],
+    "sputnik_expert_topology": [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                _P, _P, _P],
     "sputnik_can_implement": [ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_abi_block_matrix_size": [],
     "sputnik_abi_block_matrix_offset": [ctypes.c_int],
@@ -256,6 +259,26 @@ def Transpose(a: BlockMatrix, stream=None):  # noqa: N802
            "Transpose")
 
 
+def MaskToBcsr(mask, offsets, indices, stream=None):  # noqa: N802
+    """Device block mask (uint8 [R, C]) -> BCSR offsets (int32 [R+1]) and
+    ascending int16 indices (capacity >= nonzeros), the reference's
+    mask -> CSR scan (matrix_utils.cu:254-289), stream-ordered."""
+    rows, cols = int(mask.shape[0]), int(mask.shape[1])
+    _check(lib().sputnik_mask_to_bcsr(_ptr(mask), rows, cols, _ptr(offsets),
+                                      _ptr(indices), _stream(stream)),
+           "MaskToBcsr")
+
+
+def ExpertTopology(padded_bins, block_rows, blocks_per_expert, offsets,  # noqa: N802
+                   indices, stream=None):
+    """MegaBlocks dMoE topology on the device from cumulative padded bins
+    (int32 [experts]); see include/sputnik_amd.h."""
+    _check(lib().sputnik_expert_topology(
+        _ptr(padded_bins), int(padded_bins.numel()), int(block_rows),
+        int(blocks_per_expert), _ptr(offsets), _ptr(indices),
+        _stream(stream)), "ExpertTopology")
+
+
 def AllocateTransposeBuffers(a: BlockMatrix):  # noqa: N802
     """reference arguments.h:233-245 (torch-owned device workspaces)."""
     import torch
@@ -300,7 +323,8 @@ def version() -> str:
 
 __all__ = [
     "AllocateRowIndicesBuffer", "AllocateTransposeBuffers", "AsInt",
-    "BlockMatrix", "BlockSize", "FreeRowIndicesBuffer",
+    "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
+    "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",
     "SputnikError", "Transpose", "can_implement", "lib", "version",
 ]

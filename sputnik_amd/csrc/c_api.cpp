@@ -8,6 +8,7 @@
 
 #include "api_internal.h"
 #include "sputnik/sputnik.h"
+#include "metadata.h"
 #include "sputnik_amd.h"
 
 using sputnik::block::BlockMatrix;
@@ -124,6 +125,25 @@ int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream) {
       a->block_size != 16)
     return hipErrorNotSupported;
   return sputnik::block::Transpose(ToCpp(a), static_cast<hipStream_t>(stream));
+}
+
+int sputnik_mask_to_bcsr(const uint8_t *mask, int block_rows, int block_cols,
+                         int32_t *offsets, int16_t *indices, void *stream) {
+  if (!offsets || (block_rows > 0 && block_cols > 0 && (!mask || !indices)))
+    return hipErrorInvalidValue;
+  return sputnik_amd::LaunchMaskToBcsr(block_rows, block_cols, mask, offsets,
+                                       indices,
+                                       static_cast<hipStream_t>(stream));
+}
+
+int sputnik_expert_topology(const int32_t *padded_bins, int num_experts,
+                            int block_rows, int blocks_per_expert,
+                            int32_t *offsets, int16_t *indices, void *stream) {
+  if (!padded_bins || !offsets || (block_rows > 0 && !indices))
+    return hipErrorInvalidValue;
+  return sputnik_amd::LaunchExpertTopology(
+      padded_bins, num_experts, block_rows, blocks_per_expert, offsets,
+      indices, static_cast<hipStream_t>(stream));
 }
 
 int sputnik_can_implement(int op, const void *a, int transpose_a,

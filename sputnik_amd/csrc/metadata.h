@@ -14,6 +14,19 @@ hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
 hipError_t LaunchRowIndices(int block_rows, const int *offsets,
                             short *row_indices, hipStream_t stream);
 
+// Block mask (uint8 [block_rows][block_cols], nonzero = present) -> BCSR
+// offsets / ascending indices (reference matrix_utils.cu:254-289). `indices`
+// must hold the mask's nonzero count (block_rows * block_cols bounds it).
+hipError_t LaunchMaskToBcsr(int block_rows, int block_cols,
+                            const unsigned char *mask, int *offsets,
+                            short *indices, hipStream_t stream);
+
+// MegaBlocks dMoE topology from cumulative padded expert bins.
+hipError_t LaunchExpertTopology(const int *padded_bins, int num_experts,
+                                int block_rows, int blocks_per_expert,
+                                int *offsets, short *indices,
+                                hipStream_t stream);
+
 }  // namespace sputnik_amd
 
 #endif  // SPUTNIK_AMD_METADATA_H_

@@ -320,4 +320,40 @@ def from_dense_mask(x: torch.Tensor, mask) -> SparseMatrix:
                         c.to(torch.int16))
 
 
-__all__ = ["SparseMatrix", "dds", "dsd", "from_dense_mask", "sdd"]
+def topology_from_mask(mask: torch.Tensor, dtype=torch.float16
+                       ) -> SparseMatrix:
+    """SparseMatrix (uninitialised block values) whose topology is built
+    on the device from a [rows/128, cols/128] block mask."""
+    from . import MaskToBcsr
+    mask = mask.to(torch.uint8).contiguous()
+    rb, cb = mask.shape
+    offsets = torch.empty(rb + 1, dtype=torch.int32, device=mask.device)
+    cap = torch.empty(max(rb * cb, 1), dtype=torch.int16, device=mask.device)
+    MaskToBcsr(mask, offsets, cap)
+    nb = int(offsets[-1].item())  # one host sync: the block count sizes data
+    data = torch.empty(nb, BLOCK, BLOCK, dtype=dtype, device=mask.device)
+    return SparseMatrix((rb * BLOCK, cb * BLOCK), data, offsets,
+                        cap[:nb].clone())
+
+
+def expert_topology(padded_bins: torch.Tensor, blocks_per_expert: int,
+                    block_rows: int, dtype=torch.bfloat16) -> SparseMatrix:
+    """The dMoE topology (MegaBlocks `topology` op) built on the device:
+    block-row r belongs to the expert whose padded bin holds token 128 r and
+    owns that expert's `blocks_per_expert` block-columns. No host sync."""
+    from . import ExpertTopology
+    bins = padded_bins.to(torch.int32).contiguous()
+    e = int(bins.numel())
+    dev = bins.device
+    offsets = torch.empty(block_rows + 1, dtype=torch.int32, device=dev)
+    indices = torch.empty(block_rows * blocks_per_expert, dtype=torch.int16,
+                          device=dev)
+    ExpertTopology(bins, block_rows, blocks_per_expert, offsets, indices)
+    data = torch.empty(block_rows * blocks_per_expert, BLOCK, BLOCK,
+                       dtype=dtype, device=dev)
+    return SparseMatrix((block_rows * BLOCK, e * blocks_per_expert * BLOCK),
+                        data, offsets, indices)
+
+
+__all__ = ["SparseMatrix", "dds", "dsd", "expert_topology", "from_dense_mask",
+           "sdd", "topology_from_mask"]

@@ -571,6 +571,87 @@ def test_row_indices_bit_exact(shape):
 
 # ------------------------------------------------------------- errors -----
 
+@pytest.mark.parametrize("shape", [(1, 1, 1), (3, 4, 6), (32, 32, 512),
+                                   (64, 896, 7168), (300, 40, 700),
+                                   (2, 32768, 5000)])
+def test_mask_to_bcsr_bit_exact(shape):
+    """Device mask -> BCSR against the row-major scan of
+    matrix_utils.cu:254-289 (matrix_utils.mask_to_bcsr, itself checked
+    against the oracle in test_oracle.py), with an empty and a full row."""
+    rb, cb, nb = shape
+    rng = np.random.default_rng(rb * 7 + cb)
+    perm, mask = mu.random_perm_mask(rb, cb, nb, rng)
+    mask[0, :] = 0
+    if rb > 2:
+        mask[rb - 1, :] = 1
+    off_ref, idx_ref = mu.mask_to_bcsr(mask)
+    dmask = torch.from_numpy(mask.astype(np.uint8)).cuda()
+    offsets = torch.full((rb + 1,), -7, dtype=torch.int32, device="cuda")
+    indices = torch.full((rb * cb,), -7, dtype=torch.int16, device="cuda")
+    sp.MaskToBcsr(dmask, offsets, indices)
+    _sync()
+    n = int(off_ref[-1])
+    assert np.array_equal(offsets.cpu().numpy(), off_ref)
+    assert np.array_equal(indices[:n].cpu().numpy(), idx_ref.astype(np.int16))
+    assert (indices[n:].cpu().numpy() == -7).all()   # nothing past nnz
+
+
+def test_mask_to_bcsr_oracle_permutation():
+    """The oracle's permutation builder (oracle.c, matrix_utils.cu:262-289)
+    and the device builder agree bit-exactly on the same permutation."""
+    rng = np.random.default_rng(3)
+    rb, cb, nb = 48, 40, 777
+    perm, mask = mu.random_perm_mask(rb, cb, nb, rng)
+    off_o, idx_o = O.mask_to_bcsr(perm, rb, cb, nb)
+    offsets = torch.empty(rb + 1, dtype=torch.int32, device="cuda")
+    indices = torch.empty(rb * cb, dtype=torch.int16, device="cuda")
+    sp.MaskToBcsr(torch.from_numpy(mask.astype(np.uint8)).cuda(), offsets,
+                  indices)
+    _sync()
+    assert np.array_equal(offsets.cpu().numpy(), off_o)
+    assert np.array_equal(indices[:nb].cpu().numpy(), idx_o.astype(np.int16))
+
+
+@pytest.mark.parametrize("bins", [[256, 512, 768, 1024],
+                                  [128, 128, 640, 640, 1024],
+                                  [0, 384, 384, 1152]])
+def test_expert_topology(bins):
+    """dMoE topology on the device vs its numpy restatement; equal bins give
+    the expert-diagonal topology of BASELINE config 4."""
+    from sputnik_amd import ops
+    bpe = 3
+    rows_b = bins[-1] // 128
+    t = ops.expert_topology(torch.tensor(bins, dtype=torch.int32).cuda(),
+                            bpe, rows_b)
+    _sync()
+    b = np.array(bins)
+    e = np.minimum(np.searchsorted(b, np.arange(rows_b) * 128, side="right"),
+                   len(bins) - 1)
+    idx_ref = (e[:, None] * bpe + np.arange(bpe)[None, :]).reshape(-1)
+    assert np.array_equal(t.offsets.cpu().numpy(),
+                          np.arange(rows_b + 1, dtype=np.int32) * bpe)
+    assert np.array_equal(t.indices.cpu().numpy(), idx_ref.astype(np.int16))
+    assert t.shape == (rows_b * 128, len(bins) * bpe * 128)
+    if bins == [256, 512, 768, 1024]:
+        o2, i2 = mu.expert_block_diagonal(4, 2, bpe)
+        assert np.array_equal(t.indices.cpu().numpy(), i2.astype(np.int16))
+
+
+def test_topology_from_mask_feeds_products():
+    """A device-built topology drives SDD then DSD (no host metadata)."""
+    from sputnik_amd import ops
+    rng = np.random.default_rng(11)
+    _, mask = mu.random_perm_mask(3, 4, 7, rng)
+    topo = ops.topology_from_mask(torch.from_numpy(mask).cuda())
+    x = torch.rand(384, 256, device="cuda").half() - 0.5
+    w = torch.rand(256, 512, device="cuda").half() - 0.5
+    h = ops.sdd(x, w, topo)
+    full = (x.float() @ w.float())
+    m = torch.from_numpy(np.kron(mask, np.ones((128, 128)))).cuda().float()
+    H.assert_close(h.to_dense().float().cpu().numpy(),
+                   (full * m).cpu().numpy(), "f16", "sdd on device topology")
+
+
 def test_errors_returned_not_aborted():
     rng = np.random.default_rng(0)
     A = H.HostSparse(256, 256, 2 * 16384, rng)
