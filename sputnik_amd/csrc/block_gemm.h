@@ -41,6 +41,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 // Ablation switches for performance experiments only (scripts/exp_build.sh);
 // the shipped library is built with SPUTNIK_EXP == 0.
 //   1: skip the MFMAs (keep LDS reads)   2: skip the operand DMA
@@ -70,6 +72,11 @@
 // Fragment reads of the next step before this step's DMA issue.
 #ifndef SPUTNIK_READ_FIRST
 #define SPUTNIK_READ_FIRST 0
+#endif
+// DSD / DDS staggered pipeline unrolled by one stored block (constant ring
+// slots, branch-free steady state); 0 = the generic per-step pipeline.
+#ifndef SPUTNIK_BLOCK_LOOP
+#define SPUTNIK_BLOCK_LOOP 1
 #endif
 // Staggered configs: static s_setprio(1) for the lagging (younger) half.
 #ifndef SPUTNIK_LAG_PRIO
@@ -595,7 +602,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     s16x8 b[kKK][kFN];
   };
   auto read_step = [&](int slot, Frags &F) {
-    const char *simg = lds + slot * kStageBytes;
+    // Opaque slot offset: with a compile-time slot (pipeline_blocks) the
+    // compiler would otherwise hoist every slot's fragment addresses out of
+    // the loop and keep 4x the address registers live.
+    int slot_off = slot * kStageBytes;
+    asm volatile("" : "+s"(slot_off));
+    const char *simg = lds + slot_off;
     const char *dimg = simg + kSBytes;
 #pragma unroll
     for (int kk = 0; kk < kKK; ++kk) {
@@ -879,6 +891,131 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if (i + 1 < steps) body(i + 1, f1, f0);
     }
     if (Cfg::kStagger && !lag) __builtin_amdgcn_s_barrier();
+  };
+
+  // ---- DSD / DDS on the staggered configs: pipeline()'s schedule unrolled
+  // by one stored block (kStepsPerBlock = 4 steps = the 4 ring slots), so
+  // every ring slot is a compile-time constant, a block's base addresses are
+  // resolved once (its index scalar-loaded one block ahead), and the
+  // steady-state loop carries no per-step branch beyond the two uniform
+  // half-selection branches around the vmcnt waits (the leading and lagging
+  // halves differ only there; the ordering argument is pipeline()'s). Two
+  // loop copies, one per half, measured 2.4x slower: they spill the
+  // accumulators. Entries
+  // [e0, e0 + nblk) of the index segments; the pair producer publishes after
+  // block flush_blk - 1.
+  auto pipeline_blocks = [&](int e0, int nblk, int flush_blk) {
+    if (nblk <= 0) return;
+    auto entry = [&](int x) {
+      return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
+    };
+    int nk = 0, nbk = 0;  // (k-block, storage block) of the next block
+    auto load_idx = [&](int e) {
+      const int ge = entry(e);
+      nk = scalar_load_short(p.s_indices, ge);
+      nbk = p.s_block_offsets != nullptr ? scalar_load_int(p.s_block_offsets, ge)
+                                         : ge;
+    };
+    const char *cs = nullptr, *cd = nullptr;  // bases of the block being fed
+    auto take_next = [&]() {
+      cs = p.s_data + (long long)nbk * (kBlock * kBlock * 2);
+      const long long kg = (long long)nk * kBlock;
+      cd = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
+                : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+    };
+    auto fire_sub = [&](int h, int slot) {
+      s_base = cs + (kSKC ? h * (kBK * 2) : h * (kBK * 256));
+      d_base = cd + (kDKC ? (long long)h * (kBK * 2)
+                          : (long long)h * kBK * p.d_ld);
+      fire(slot);
+    };
+    load_idx(e0);
+    take_next();
+    fire_sub(0, 0);
+    fire_sub(1, 1);
+    fire_sub(2, 2);
+    load_idx(e0 + min(1, nblk - 1));  // prefetch block 1
+    wait_vmcnt<2 * kGroup>();
+    __builtin_amdgcn_s_barrier();
+    Frags f0, f1;
+    read_step(0, f0);
+    wait_step(f0);
+    exp_stamp(p.debug, 8, __builtin_amdgcn_s_memtime());
+    const bool lag = wave >= kNW / 2;
+    if constexpr (SPUTNIK_LAG_PRIO != 0) {
+      if (lag) __builtin_amdgcn_s_setprio(1);
+    }
+    if (lag) {
+      wait_vmcnt<kGroup>();
+      __builtin_amdgcn_s_barrier();
+    }
+    // Step h of block b (i = 4b + h of s = 4 nblk steps): LAST marks the
+    // final block, where pipeline()'s end conditions apply.
+    auto step = [&](auto h_c, auto last_c, int b, Frags &cur, Frags &next) {
+      const bool L = lag;
+      constexpr int H = decltype(h_c)::value;
+      constexpr bool LAST = decltype(last_c)::value;
+      constexpr bool kHasNext = !(LAST && H == 3);        // i + 1 < s
+      if constexpr (kHasNext) {
+        if (!L) {
+          if constexpr (LAST && H == 2)
+            wait_vmcnt<0>();
+          else
+            wait_vmcnt<kGroup>();
+        }
+        __builtin_amdgcn_s_barrier();
+        if constexpr (H == 0) {
+          fire_sub(3, 3);                                   // step i + 3
+        } else if constexpr (!LAST) {
+          if constexpr (H == 1) {
+            take_next();
+            load_idx(e0 + min(b + 2, nblk - 1));            // block b + 2
+          }
+          fire_sub(H - 1, H - 1);
+        }
+        read_step((H + 1) & 3, next);
+      }
+      if (L) {
+        if constexpr (!LAST || H == 0)
+          wait_vmcnt<kGroup>();
+        else if constexpr (H == 1)
+          wait_vmcnt<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      mfma_step(cur);
+      if constexpr (kHasNext) wait_step(next);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    auto run = [&]() {
+      int b = 0;
+      for (; b + 1 < nblk; ++b) {
+        step(I0{}, std::false_type{}, b, f0, f1);
+        step(I1{}, std::false_type{}, b, f1, f0);
+        step(I2{}, std::false_type{}, b, f0, f1);
+        step(I3{}, std::false_type{}, b, f1, f0);
+        if constexpr (kPairs) {
+          if (b + 1 == flush_blk) {
+            publish();
+            exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
+          }
+        }
+      }
+      step(I0{}, std::true_type{}, b, f0, f1);
+      step(I1{}, std::true_type{}, b, f1, f0);
+      step(I2{}, std::true_type{}, b, f0, f1);
+      step(I3{}, std::true_type{}, b, f1, f0);
+      if constexpr (kPairs) {
+        if (b + 1 == flush_blk) {
+          publish();
+          exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
+        }
+      }
+    };
+    run();
+    if (!lag) __builtin_amdgcn_s_barrier();
   };
 
   // Steps [s_begin, s_end) of sparse block-row `srow` whose entries start at
@@ -1254,7 +1391,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   } else if constexpr (kScalarIdx) {
     exp_stamp(p.debug, 7, p_steps);
     cached_e = -1;
-    pipeline(p_first, p_steps, p_flush);
+    // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
+    // needs 12 more address registers than it has and spills; those two
+    // keep the per-step pipeline.)
+    if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger && kStages == 4 &&
+                  kStepsPerBlock == 4 && !(kSKC && kDKC))
+      pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
+                      p_flush > 0 ? p_flush / kStepsPerBlock : -1);
+    else
+      pipeline(p_first, p_steps, p_flush);
     exp_stamp(p.debug, 10, __builtin_amdgcn_s_memtime());
     if (do_collect) collect();
     exp_stamp(p.debug, 11, __builtin_amdgcn_s_memtime());
