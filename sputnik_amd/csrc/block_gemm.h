@@ -78,6 +78,10 @@
 #ifndef SPUTNIK_BLOCK_LOOP
 #define SPUTNIK_BLOCK_LOOP 1
 #endif
+// The same block loop for the grouped SDD (groups of 4 k-steps).
+#ifndef SPUTNIK_SDD_BLOCK_LOOP
+#define SPUTNIK_SDD_BLOCK_LOOP 1
+#endif
 // Staggered configs: static s_setprio(1) for the lagging (younger) half.
 #ifndef SPUTNIK_LAG_PRIO
 #define SPUTNIK_LAG_PRIO 1
@@ -929,12 +933,21 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                           : (long long)h * kBK * p.d_ld);
       fire(slot);
     };
-    load_idx(e0);
-    take_next();
-    fire_sub(0, 0);
-    fire_sub(1, 1);
-    fire_sub(2, 2);
-    load_idx(e0 + min(1, nblk - 1));  // prefetch block 1
+    if constexpr (kSparseOut) {  // SDD: step s covers k = 32 s ..
+      prep(0);
+      fire(0);
+      prep(1);
+      fire(1);
+      prep(2);
+      fire(2);
+    } else {
+      load_idx(e0);
+      take_next();
+      fire_sub(0, 0);
+      fire_sub(1, 1);
+      fire_sub(2, 2);
+      load_idx(e0 + min(1, nblk - 1));  // prefetch block 1
+    }
     wait_vmcnt<2 * kGroup>();
     __builtin_amdgcn_s_barrier();
     Frags f0, f1;
@@ -964,7 +977,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
             wait_vmcnt<kGroup>();
         }
         __builtin_amdgcn_s_barrier();
-        if constexpr (H == 0) {
+        if constexpr (kSparseOut) {
+          if constexpr (H == 0 || !LAST) {                  // step i + 3
+            prep(4 * b + H + 3);
+            fire((H + 3) & 3);
+          }
+        } else if constexpr (H == 0) {
           fire_sub(3, 3);                                   // step i + 3
         } else if constexpr (!LAST) {
           if constexpr (H == 1) {
@@ -1387,7 +1405,13 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   if constexpr (kSparseOut) {
     const int nsteps = (p.k_limit + kBK - 1) / kBK;
     exp_stamp(p.debug, 7, nsteps);
-    pipeline(0, nsteps);
+    // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
+    // zeros through the k mask (at most 3, none when K % 128 == 0).
+    if constexpr (SPUTNIK_SDD_BLOCK_LOOP != 0 && Cfg::kStagger &&
+                  kStages == 4)
+      pipeline_blocks(0, (nsteps + 3) / 4, -1);
+    else
+      pipeline(0, nsteps);
   } else if constexpr (kScalarIdx) {
     exp_stamp(p.debug, 7, p_steps);
     cached_e = -1;
