@@ -1166,6 +1166,46 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // Rows of rank ra and rb (rank 0 = most nonzeros, ties by row index), one
   // parallel pass over the offsets staged in LDS (R <= kLptRows). The ring
   // is free again on return.
+  // Same ranking for R < 64 rows, barrier-free: every wave computes it on
+  // its own, lane r holding row r (n_r by readlane broadcast, R steps), the
+  // rank -> length table in a per-wave LDS scratch inside ring slot 3 (on
+  // the staggered 4-slot configs, slot 3 is not written before every wave
+  // has passed the pipeline's first barrier).
+  // Returns (row of rank ra, row of rank rb) and their (first entry, count).
+  struct RowPick { int row_a, row_b, e_a, n_a, e_b, n_b; };
+  auto rank_rows_wave = [&](int ra, int rb) {
+    const int R = p.num_rows;
+    const int o0 = lane <= R ? p.s_offsets[lane] : 0;
+    const int o1 = __shfl_down(o0, 1, 64);
+    const int nr = lane < R ? o1 - o0 : -1;
+    int rank = 0;
+    for (int r2 = 0; r2 < R; ++r2) {
+      const int n2 = __builtin_amdgcn_readlane(nr, r2);
+      rank += (n2 > nr) | ((n2 == nr) & (r2 < lane));
+    }
+    const bool live = lane < R;
+    const unsigned long long ba = __ballot(live && rank == ra);
+    const unsigned long long bb = __ballot(live && rank == rb);
+    RowPick out;
+    out.row_a = __builtin_ctzll(ba);
+    out.row_b = __builtin_ctzll(bb);
+    out.e_a = __builtin_amdgcn_readlane(o0, out.row_a);
+    out.n_a = __builtin_amdgcn_readlane(nr, out.row_a);
+    out.e_b = __builtin_amdgcn_readlane(o0, out.row_b);
+    out.n_b = __builtin_amdgcn_readlane(nr, out.row_b);
+    // Pair target: max over i of ceil((n[rank i] + n[rank R-1-i]) / 2).
+    int *nbr = reinterpret_cast<int *>(lds + 3 * kStageBytes + wave * 256);
+    if (live) nbr[rank] = nr;
+    int v = 0;
+    if (lane < (R + 1) / 2) {
+      const int j = R - 1 - lane;
+      v = lane == j ? nbr[lane] : (nbr[lane] + nbr[j] + 1) / 2;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d, 64));
+    pair_target = __builtin_amdgcn_readfirstlane(v);
+    return out;
+  };
   auto rank_rows = [&](int ra, int rb) {
     const int R = p.num_rows;
     int *offs = reinterpret_cast<int *>(lds);
@@ -1247,15 +1287,23 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       panel = t / half;
       pi = t % half;
     }
-    const int2 rows = rank_rows(pi, R - 1 - pi);
-    // The offsets are still staged in LDS by rank_rows (the ring is not
-    // written before the first DMA): no dependent global round trip.
-    const int *offs = reinterpret_cast<const int *>(lds);
-    const int e_h = __builtin_amdgcn_readfirstlane(offs[rows.x]);
-    const int n_h = __builtin_amdgcn_readfirstlane(offs[rows.x + 1]) - e_h;
-    const int e_l = __builtin_amdgcn_readfirstlane(offs[rows.y]);
-    const int n_l = __builtin_amdgcn_readfirstlane(offs[rows.y + 1]) - e_l;
-    __syncthreads();  // staged offsets / scratch read by every wave
+    int2 rows;
+    int e_h, n_h, e_l, n_l;
+    if (Cfg::kStagger && R < 64) {
+      const RowPick rp = rank_rows_wave(pi, R - 1 - pi);
+      rows = make_int2(rp.row_a, rp.row_b);
+      e_h = rp.e_a; n_h = rp.n_a; e_l = rp.e_b; n_l = rp.n_b;
+    } else {
+      rows = rank_rows(pi, R - 1 - pi);
+      // The offsets are still staged in LDS by rank_rows (the ring is not
+      // written before the first DMA): no dependent global round trip.
+      const int *offs = reinterpret_cast<const int *>(lds);
+      e_h = __builtin_amdgcn_readfirstlane(offs[rows.x]);
+      n_h = __builtin_amdgcn_readfirstlane(offs[rows.x + 1]) - e_h;
+      e_l = __builtin_amdgcn_readfirstlane(offs[rows.y]);
+      n_l = __builtin_amdgcn_readfirstlane(offs[rows.y + 1]) - e_l;
+      __syncthreads();  // staged offsets / scratch read by every wave
+    }
     // Hand over only what exceeds the panel's balanced target, and nothing
     // under kMinHandoff blocks: a hand-off costs each side about one
     // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
@@ -1385,11 +1433,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       j0 = panel * kBN;
       srow = target;
       if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
-        srow = rank_rows(target, target).x;
-        const int *offs = reinterpret_cast<const int *>(lds);  // staged
-        entry0 = __builtin_amdgcn_readfirstlane(offs[srow]);
-        entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
-        __syncthreads();  // staged offsets / scratch read by every wave
+        if (Cfg::kStagger && p.num_rows < 64) {
+          const RowPick rp = rank_rows_wave(target, target);
+          srow = rp.row_a;
+          entry0 = rp.e_a;
+          entries = rp.n_a;
+        } else {
+          srow = rank_rows(target, target).x;
+          const int *offs = reinterpret_cast<const int *>(lds);  // staged
+          entry0 = __builtin_amdgcn_readfirstlane(offs[srow]);
+          entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
+          __syncthreads();  // staged offsets / scratch read by every wave
+        }
       } else {
         entry0 = p.s_offsets[srow];
         entries = p.s_offsets[srow + 1] - entry0;
