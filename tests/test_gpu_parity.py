@@ -333,6 +333,55 @@ def run_sdd(p, dtype="f16", seed=0):
     return gpu_blocks, ref_blocks
 
 
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("k", [1024, 1032, 2056])
+def test_sdd_long_ragged_k(ta, tb, k):
+    """SDD with long, ragged K (an odd number of 64-deep steps and a partial
+    last step) on every transpose, unordered indices, against the oracle."""
+    p = dict(m=512, k=k, n=640, nonzeros=9 * 16384, ta=ta, tb=tb,
+             unordered=True)
+    gpu, ref = run_sdd(p, seed=k)
+    H.assert_close(gpu, ref, "f16", "sdd long k")
+    if not ta and not tb:
+        gpu, ref = run_sdd(p, dtype="bf16", seed=k + 1)
+        H.assert_close(gpu, ref, "bf16", "sdd long k bf16")
+
+
+def test_sdd_repeat_and_graph():
+    """Repeated SDD calls and a captured graph replayed several times give
+    identical bits."""
+    p = dict(m=384, k=2048, n=512, nonzeros=7 * 16384, ta=False, tb=False,
+             unordered=False)
+    rng = np.random.default_rng(3)
+    A = H.HostDense(384, 2048, rng)
+    B = H.HostDense(2048, 512, rng)
+    Cs = H.HostSparse(384, 512, p["nonzeros"], rng)
+    sp.AllocateRowIndicesBuffer(Cs.matrix)
+    sp.RowIndices(Cs.matrix, Cs.matrix.row_indices)
+    sp.Matmul(A.matrix, False, B.matrix, False, Cs.matrix)
+    _sync()
+    first = Cs.dev_values.clone()
+    for _ in range(5):
+        sp.Matmul(A.matrix, False, B.matrix, False, Cs.matrix)
+    _sync()
+    assert torch.equal(Cs.dev_values, first)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # eager call on s: its workspace exists
+        sp.Matmul(A.matrix, False, B.matrix, False, Cs.matrix)
+    torch.cuda.current_stream().wait_stream(s)
+    _sync()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.Matmul(A.matrix, False, B.matrix, False, Cs.matrix)
+    for _ in range(4):
+        Cs.dev_values.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(Cs.dev_values, first)
+
+
 @pytest.mark.parametrize("p", _problems("sdd"))
 def test_sdd_reference_problems(p):
     gpu, ref = run_sdd(p)
