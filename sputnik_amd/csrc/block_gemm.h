@@ -227,9 +227,12 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
   const int sector = col0 >> 4;
   s16x4 lo, hi;
   const int k = 32 * kk + 8 * g + q;
-  const uint32_t addr = (uint32_t)(uintptr_t)(
-      (__attribute__((address_space(3))) const char *)(
-          img + k * kRowBytes + ((sector ^ tr_key(k)) << 5) + (p << 3)));
+  // (image + lane's row/piece) is shared by every fragment of a step, the
+  // swizzled sector term is loop-invariant: one add per fragment per step.
+  const uint32_t row_base = (uint32_t)(uintptr_t)(
+      (__attribute__((address_space(3))) const char *)(img)) +
+      (uint32_t)(k * kRowBytes + (p << 3));
+  const uint32_t addr = row_base + (uint32_t)((sector ^ tr_key(k)) << 5);
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(addr));
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
                : "=v"(hi)
