@@ -1,6 +1,7 @@
 // sputnik-amd umbrella header. Replaces reference sputnik/sputnik.h:18-25 for
-// the block-sparse hot path (DSD, DDS, SDD, RowIndices). SSD/SDS/DSS are out of
-// scope and are not declared.
+// the block-sparse products (DSD, DDS, SDD, SSD, SDS) and the metadata
+// builders (RowIndices, Transpose). DSS (sparse x sparse via bitmask
+// intersection) is not declared.
 #ifndef SPUTNIK_SPUTNIK_H_
 #define SPUTNIK_SPUTNIK_H_
 
@@ -8,6 +9,8 @@
 #include "sputnik/block/dsd/dsd.h"
 #include "sputnik/block/dds/dds.h"
 #include "sputnik/block/sdd/sdd.h"
+#include "sputnik/block/ssd/ssd.h"
+#include "sputnik/block/sds/sds.h"
 #include "sputnik/block/row_indices/row_indices.h"
 #include "sputnik/block/transpose/transpose.h"
 

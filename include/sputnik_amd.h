@@ -78,6 +78,26 @@ int sputnik_sdd(const sputnik_matrix_t *a, int transpose_a,
                 const sputnik_matrix_t *b, int transpose_b,
                 const sputnik_block_matrix_t *c, int dtype, void *stream);
 
+/* ---- SSD: C_bcsr = op(A_bcsr) * op(B) at C's nonzero blocks
+ *      (reference sputnik/block/ssd/ssd.h:10-22; needs c->row_indices, and
+ *      a's transposed metadata when transpose_a) */
+int sputnik_ssd(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream);
+int sputnik_ssd_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_matrix_t *b, int transpose_b,
+                   const sputnik_block_matrix_t *c, int dtype, void *stream);
+
+/* ---- SDS: C_bcsr = op(A) * op(B_bcsr) at C's nonzero blocks
+ *      (reference sputnik/block/sds/sds.h:10-22; needs c->row_indices, and
+ *      b's transposed metadata when !transpose_b) */
+int sputnik_sds(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream);
+int sputnik_sds_ex(const sputnik_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_block_matrix_t *c, int dtype, void *stream);
+
 /* ---- Metadata builders */
 /* reference sputnik/block/row_indices/row_indices.h:10 */
 int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,

@@ -30,10 +30,17 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
                   const BlockMatrix &c, int dtype, hipStream_t stream,
                   Status *status);
 
+hipError_t RunSsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *status);
+hipError_t RunSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *status);
+
 // hipError_t value the C-ABI returns for a status (never aborts).
 int StatusCode(Status st);
 
-// Host-only acceptance test. op 0 = DSD, 1 = DDS, 2 = SDD.
+// Host-only acceptance test. op 0 = DSD, 1 = DDS, 2 = SDD, 3 = SSD, 4 = SDS.
 bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
                   const void *c);
 

@@ -334,11 +334,14 @@ using CfgSdd = SPUTNIK_SDD_CFG;        // SDD tile configuration (BN = 128)
 // guard, not part of the protocol.
 constexpr int kSpinLimit = 1 << 22;
 
-// kSparseOut: SDD (dense S, sparse output block); else DSD/DDS (sparse S).
+// kSparseOut: sparse output block. With kSparseIn = false that is SDD (dense
+// S); with kSparseIn = true, SSD / SDS (sparse S, as DSD / DDS, restricted to
+// the output's nonzero blocks: one 128x128 block per workgroup). Without
+// kSparseOut: DSD / DDS (sparse S, dense output).
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
 // kOutT: write O transposed (DDS).
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
-          class Cfg>
+          class Cfg, bool kSparseIn = false>
 __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                                   Cfg::kWGs * Cfg::kWM * Cfg::kWN / 4)
     block_gemm_kernel(const GemmParams p) {
@@ -371,12 +374,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // a CU); staggered configs read it with scalar loads instead.
   constexpr bool kScalarIdx = Cfg::kStagger;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
+  constexpr bool kDenseS = kSparseOut && !kSparseIn;  // SDD
+  static_assert(!kSparseIn || (kSparseOut && !Cfg::kStagger && kBN == kBlock),
+                "SSD/SDS: one output block per workgroup, per-step pipeline");
   constexpr int kIdxBytes =
-      kSparseOut ? (Cfg::kStagger ? 0 : 16)
+      kDenseS ? (Cfg::kStagger ? 0 : 16)
                  : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
   // SDD with kBN > 128: a tile is a group of up to kGrp stored blocks of one
   // block-row, found in-kernel from C's offsets (rows <= kMaxGroupRows).
-  constexpr bool kGroupedSdd = kSparseOut && kBN > kBlock;
+  constexpr bool kGroupedSdd = kDenseS && kBN > kBlock;
   constexpr int kGrp = kBN / kBlock;
   static_assert(!Cfg::kStagger || kStages >= 4, "stagger needs 4 slots");
   static_assert(!Cfg::kStagger || (Cfg::kWM * Cfg::kWN) % 2 == 0, "halves");
@@ -416,7 +422,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   // ---- per-lane DMA offsets (relative to each step's tile base) ----------
   uint32_t s_off[kSInstr], d_off[kDInstr];
   int s_lk[kSInstr], d_lk[kDInstr];  // k of the lane's chunk (SDD k-mask)
-  const long long s_stride = kSparseOut ? p.s_ld : 256;
+  const long long s_stride = kDenseS ? p.s_ld : 256;
 #pragma unroll
   for (int q = 0; q < kSInstr; ++q) {
     const int g = wave * kSInstr + q;
@@ -513,7 +519,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   auto prep = [&](int step) {
     if constexpr ((SPUTNIK_EXP & 2) != 0) return;
     if constexpr ((SPUTNIK_EXP & 64) != 0) step = 0;
-    if constexpr (kSparseOut) {
+    if constexpr (kDenseS) {
       const long long k0 = (long long)step * kBK;
       krem = p.k_limit - (int)k0;
       s_base = kSKC ? p.s_data + (long long)srow * kBM * p.s_ld + k0 * 2
@@ -585,14 +591,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 #pragma unroll
     for (int q = 0; q < kSInstr; ++q) {
       uint32_t off = s_off[q];
-      if constexpr (kSparseOut) off = s_lk[q] < krem ? off : kOOB;
-      dma16<kSparseOut ? 0 : SPUTNIK_S_AUX>(
+      if constexpr (kDenseS) off = s_lk[q] < krem ? off : kOOB;
+      dma16<kDenseS ? 0 : SPUTNIK_S_AUX>(
           rs, slot_base + (wave * kSInstr + q) * 1024, off);
     }
 #pragma unroll
     for (int q = 0; q < kDInstr; ++q) {
       uint32_t off = d_off[q];
-      if constexpr (kSparseOut) off = d_lk[q] < krem ? off : kOOB;
+      if constexpr (kDenseS) off = d_lk[q] < krem ? off : kOOB;
       dma16<SPUTNIK_D_AUX>(rd, slot_base + kSBytes + (wave * kDInstr + q) * 1024,
                            off);
     }
@@ -936,7 +942,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                           : (long long)h * kBK * p.d_ld);
       fire(slot);
     };
-    if constexpr (kSparseOut) {  // SDD: step s covers k = 32 s ..
+    if constexpr (kDenseS) {  // SDD: step s covers k = 32 s ..
       prep(0);
       fire(0);
       prep(1);
@@ -980,7 +986,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
             wait_vmcnt<kGroup>();
         }
         __builtin_amdgcn_s_barrier();
-        if constexpr (kSparseOut) {
+        if constexpr (kDenseS) {
           if constexpr (H == 0 || !LAST) {                  // step i + 3
             prep(4 * b + H + 3);
             fire((H + 3) & 3);
@@ -1144,7 +1150,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
         const uint4 v =
             *reinterpret_cast<const uint4 *>(st + row * kStLd + cc * 16);
         char *dst;
-        if constexpr (kSparseOut) {
+        if constexpr (kSparseOut && kOutT) {
+          // SDS: the tile is the block transposed; staging row j is row j
+          // of the output block.
+          dst = p.c_data + out_block * (kBlock * kBlock * 2) +
+                (jp0 + row) * (kBlock * 2) + cc * 16;
+        } else if constexpr (kSparseOut) {
           const int jcol = jp0 + cc * 8;  // column inside the tile
           const int jb = jcol / kBlock;
           if (jb >= grp_count) continue;
@@ -1417,6 +1428,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if (kGrp > 2 && grp_count > 2) grp_c2 = p.c_indices[b0 + 2] * kBlock;
       if (kGrp > 3 && grp_count > 3) grp_c3 = p.c_indices[b0 + 3] * kBlock;
       __syncthreads();  // wsum / scratch reads done before the ring is used
+    } else if constexpr (kSparseIn) {
+      // SSD: block (r, c) of C is row r of op(A) times column panel c of
+      // op(B). SDS computes the block transposed: row c of op(B)^T times
+      // row panel r of op(A)^T.
+      out_block = tile;
+      grp_b0 = tile;
+      const int r = p.c_row_indices[tile];
+      const int c = p.c_indices[tile];
+      srow = kOutT ? c : r;
+      j0 = (kOutT ? r : c) * kBlock;
+      entry0 = p.s_offsets[srow];
+      entries = p.s_offsets[srow + 1] - entry0;
     } else if constexpr (kSparseOut) {
       out_block = tile;
       grp_b0 = tile;
@@ -1460,7 +1483,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   setup_d(j0);
   zero_acc();
   exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
-  if constexpr (kSparseOut) {
+  if constexpr (kDenseS) {
     const int nsteps = (p.k_limit + kBK - 1) / kBK;
     exp_stamp(p.debug, 7, nsteps);
     // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
@@ -1521,6 +1544,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
                            bool out_t, bool grouped, const GemmParams &params,
                            hipStream_t stream);
+// SSD (out_t = false) / SDS (out_t = true) on CfgBlock: num_tiles = C's
+// nonzero blocks.
+hipError_t LaunchBlockGemmSparseIn(int dtype, bool s_kc, bool d_kc, bool out_t,
+                                   const GemmParams &params,
+                                   hipStream_t stream);
 
 }  // namespace sputnik_amd
 

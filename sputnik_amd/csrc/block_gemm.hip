@@ -60,7 +60,39 @@ hipError_t LaunchTyped(bool sparse_out, bool s_kc, bool d_kc, bool out_t,
   }
 }
 
+template <typename T>
+hipError_t LaunchSparseIn(bool s_kc, bool d_kc, bool out_t,
+                          const GemmParams &p, hipStream_t stream) {
+  if (p.num_tiles <= 0) return hipSuccess;
+  const int code = (s_kc ? 4 : 0) | (d_kc ? 2 : 0) | (out_t ? 1 : 0);
+#define SPUTNIK_SS(SKC, DKC, OUTT)                                         \
+  hipLaunchKernelGGL(                                                      \
+      (block_gemm_kernel<T, true, SKC, DKC, OUTT, CfgBlock, true>),       \
+      dim3(p.num_tiles), dim3(64 * CfgBlock::kWM * CfgBlock::kWN), 0,     \
+      stream, p);                                                          \
+  return hipGetLastError()
+  switch (code) {
+    case 4: SPUTNIK_SS(true, false, false);   // SSD NN
+    case 6: SPUTNIK_SS(true, true, false);    // SSD NT
+    case 0: SPUTNIK_SS(false, false, false);  // SSD TN
+    case 2: SPUTNIK_SS(false, true, false);   // SSD TT
+    case 3: SPUTNIK_SS(false, true, true);    // SDS NN
+    case 7: SPUTNIK_SS(true, true, true);     // SDS NT
+    case 1: SPUTNIK_SS(false, false, true);   // SDS TN
+    default: SPUTNIK_SS(true, false, true);   // SDS TT
+  }
+#undef SPUTNIK_SS
+}
+
 }  // namespace
+
+hipError_t LaunchBlockGemmSparseIn(int dtype, bool s_kc, bool d_kc, bool out_t,
+                                   const GemmParams &params,
+                                   hipStream_t stream) {
+  if (dtype == 1)
+    return LaunchSparseIn<__bf16>(s_kc, d_kc, out_t, params, stream);
+  return LaunchSparseIn<_Float16>(s_kc, d_kc, out_t, params, stream);
+}
 
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
                            bool out_t, bool grouped, const GemmParams &params,

@@ -108,6 +108,59 @@ int sputnik_sdd(const sputnik_matrix_t *a, int transpose_a,
   return Code(e, sputnik_amd::StatusCode(st));
 }
 
+static int SparseInOut(bool ssd, bool ex, const void *a, int ta,
+                       const void *b, int tb,
+                       const sputnik_block_matrix_t *c, int dtype,
+                       void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  sputnik_amd::Status st;
+  hipError_t e;
+  if (ssd) {
+    BlockMatrix ca = ToCpp(static_cast<const sputnik_block_matrix_t *>(a));
+    if (ex) ca.create_metadata = false;
+    e = sputnik_amd::RunSsd(ca, ta != 0,
+                            ToCpp(static_cast<const sputnik_matrix_t *>(b)),
+                            tb != 0, ToCpp(c), dtype, ca.create_metadata,
+                            static_cast<hipStream_t>(stream), &st);
+  } else {
+    BlockMatrix cb = ToCpp(static_cast<const sputnik_block_matrix_t *>(b));
+    if (ex) cb.create_metadata = false;
+    e = sputnik_amd::RunSds(ToCpp(static_cast<const sputnik_matrix_t *>(a)),
+                            ta != 0, cb, tb != 0, ToCpp(c), dtype,
+                            cb.create_metadata,
+                            static_cast<hipStream_t>(stream), &st);
+  }
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_ssd(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream) {
+  return SparseInOut(true, false, a, transpose_a, b, transpose_b, c, dtype,
+                     stream);
+}
+
+int sputnik_ssd_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_matrix_t *b, int transpose_b,
+                   const sputnik_block_matrix_t *c, int dtype, void *stream) {
+  return SparseInOut(true, true, a, transpose_a, b, transpose_b, c, dtype,
+                     stream);
+}
+
+int sputnik_sds(const sputnik_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_block_matrix_t *c, int dtype, void *stream) {
+  return SparseInOut(false, false, a, transpose_a, b, transpose_b, c, dtype,
+                     stream);
+}
+
+int sputnik_sds_ex(const sputnik_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_block_matrix_t *c, int dtype, void *stream) {
+  return SparseInOut(false, true, a, transpose_a, b, transpose_b, c, dtype,
+                     stream);
+}
+
 int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
                         void *stream) {
   if (!a || (!row_indices && a->nonzeros > 0)) return hipErrorInvalidValue;

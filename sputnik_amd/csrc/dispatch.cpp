@@ -251,6 +251,79 @@ Status PrepareSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   return Status::kOk;
 }
 
+// SSD / SDS: a sparse operand as in DSD / DDS, a sparse output as in SDD
+// (reference ssd.cu:7-24 and sds.cu:7-24; their *_align8.cu variants need
+// the sparse input's transposed metadata exactly where DSD / DDS do, and
+// c.row_indices always).
+Status PrepareSparseOut(const BlockMatrix &c, GemmParams *p) {
+  if (c.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(c)) return Status::kNoKernel;
+  const int blocks = c.nonzeros / (kBlock * kBlock);
+  if (blocks > 0 && c.row_indices == nullptr)
+    return Status::kMissingRowIndices;
+  p->c_data = static_cast<char *>(c.data);
+  p->c_row_indices = static_cast<const short *>(c.row_indices);
+  p->c_indices = static_cast<const short *>(c.indices);
+  p->num_tiles = blocks;
+  return Status::kOk;
+}
+
+Status PrepareSsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, GemmParams *p, bool *needs_meta) {
+  if (a.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(a) || !DenseOk(b)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s)) return Status::kNoKernel;
+  if (!StrideOk(tb ? kBlock : 64, s.ldb)) return Status::kNoKernel;
+  *needs_meta = ta;
+  if (ta && (a.offsets_t == nullptr || a.indices_t == nullptr ||
+             a.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+  *p = GemmParams{};
+  const Status st = PrepareSparseOut(c, p);
+  if (st != Status::kOk) return st;
+  p->s_data = static_cast<const char *>(a.data);
+  p->s_offsets = static_cast<const int *>(ta ? a.offsets_t : a.offsets);
+  p->s_indices = static_cast<const short *>(ta ? a.indices_t : a.indices);
+  p->s_block_offsets =
+      ta ? static_cast<const int *>(a.block_offsets) : nullptr;
+  p->d_data = static_cast<const char *>(b.data);
+  p->d_ld = (long long)s.ldb * 2;
+  p->num_rows = s.m / kBM;
+  p->j_limit = s.n;
+  return Status::kOk;
+}
+
+Status PrepareSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const BlockMatrix &c, GemmParams *p, bool *needs_meta) {
+  if (b.block_size != BlockSize::k128) return Status::kNotSupported;
+  if (!SparseOk(b) || !DenseOk(a)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s)) return Status::kNoKernel;
+  if (!StrideOk(!ta ? kBlock : 64, s.lda)) return Status::kNoKernel;
+  const bool col_order = !tb;
+  *needs_meta = col_order;
+  if (col_order && (b.offsets_t == nullptr || b.indices_t == nullptr ||
+                    b.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+  *p = GemmParams{};
+  const Status st = PrepareSparseOut(c, p);
+  if (st != Status::kOk) return st;
+  p->s_data = static_cast<const char *>(b.data);
+  p->s_offsets = static_cast<const int *>(col_order ? b.offsets_t : b.offsets);
+  p->s_indices =
+      static_cast<const short *>(col_order ? b.indices_t : b.indices);
+  p->s_block_offsets =
+      col_order ? static_cast<const int *>(b.block_offsets) : nullptr;
+  p->d_data = static_cast<const char *>(a.data);
+  p->d_ld = (long long)s.lda * 2;
+  p->num_rows = s.n / kBM;
+  p->j_limit = s.m;
+  return Status::kOk;
+}
+
 hipError_t BuildTransposed(const BlockMatrix &a, hipStream_t stream) {
   const int b = AsInt(a.block_size);
   if (b == 0) return hipErrorNotSupported;
@@ -390,6 +463,40 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
                          grouped, p, stream);
 }
 
+hipError_t RunSsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *st_out) {
+  GemmParams p;
+  bool needs_meta = false;
+  const Status st = PrepareSsd(a, ta, b, tb, c, &p, &needs_meta);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  if (needs_meta && build_meta) {
+    const hipError_t e = BuildTransposed(a, stream);
+    if (e != hipSuccess) return e;
+  }
+  p.debug = g_debug;
+  return LaunchBlockGemmSparseIn(dtype, /*s_kc=*/!ta, /*d_kc=*/tb,
+                                 /*out_t=*/false, p, stream);
+}
+
+hipError_t RunSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const BlockMatrix &c, int dtype, bool build_meta,
+                  hipStream_t stream, Status *st_out) {
+  GemmParams p;
+  bool needs_meta = false;
+  const Status st = PrepareSds(a, ta, b, tb, c, &p, &needs_meta);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  if (needs_meta && build_meta) {
+    const hipError_t e = BuildTransposed(b, stream);
+    if (e != hipSuccess) return e;
+  }
+  p.debug = g_debug;
+  return LaunchBlockGemmSparseIn(dtype, /*s_kc=*/tb, /*d_kc=*/!ta,
+                                 /*out_t=*/true, p, stream);
+}
+
 }  // namespace sputnik_amd
 
 // ---- C++ API (drop-in for the reference's sputnik::block) ---------------
@@ -469,6 +576,63 @@ hipError_t Matmul(const Matrix a, bool transpose_a, const Matrix b,
   return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
 }
 
+// SSD (reference sputnik/block/ssd/ssd.h:10-22) and SDS (sds.h:10-22).
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, BlockMatrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e =
+      sputnik_amd::RunSsd(a, transpose_a, b, transpose_b, c, (int)dtype,
+                          a.create_metadata, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "ssd");
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const Matrix b,
+                    bool transpose_b, BlockMatrix c, DataType dtype,
+                    hipStream_t stream) {
+  BlockMatrix acp = a;
+  acp.create_metadata = false;
+  return Matmul(acp, transpose_a, b, transpose_b, c, dtype, stream);
+}
+
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const Matrix b,
+                  bool transpose_b, BlockMatrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const Matrix b,
+                    bool transpose_b, BlockMatrix c, hipStream_t stream) {
+  return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, BlockMatrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e =
+      sputnik_amd::RunSds(a, transpose_a, b, transpose_b, c, (int)dtype,
+                          b.create_metadata, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "sds");
+}
+
+hipError_t MatmulEx(const Matrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, BlockMatrix c, DataType dtype,
+                    hipStream_t stream) {
+  BlockMatrix bcp = b;
+  bcp.create_metadata = false;
+  return Matmul(a, transpose_a, bcp, transpose_b, c, dtype, stream);
+}
+
+hipError_t Matmul(const Matrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, BlockMatrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t MatmulEx(const Matrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, BlockMatrix c, hipStream_t stream) {
+  return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
 hipError_t RowIndices(BlockMatrix a, short *row_indices, hipStream_t stream) {
   if (AsInt(a.block_size) == 0) return hipErrorNotSupported;
   return sputnik_amd::LaunchRowIndices(a.rows / AsInt(a.block_size),
@@ -495,7 +659,8 @@ namespace sputnik_amd {
 int StatusCode(Status st) { return AsCode(st); }
 
 // Host-only acceptance test (no launch, no device needed): op 0 = DSD
-// (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block). The C
+// (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block), 3 = SSD
+// (a, c: block), 4 = SDS (b, c: block). The C
 // descriptors share the C++ layout (static_asserts in c_api.cpp).
 bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
                   const void *c) {
@@ -515,6 +680,14 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
     st = PrepareSdd(*static_cast<const Matrix *>(a), ta,
                     *static_cast<const Matrix *>(b), tb,
                     *static_cast<const BlockMatrix *>(c), &p);
+  } else if (op == 3) {
+    st = PrepareSsd(*static_cast<const BlockMatrix *>(a), ta,
+                    *static_cast<const Matrix *>(b), tb,
+                    *static_cast<const BlockMatrix *>(c), &p, &meta);
+  } else if (op == 4) {
+    st = PrepareSds(*static_cast<const Matrix *>(a), ta,
+                    *static_cast<const BlockMatrix *>(b), tb,
+                    *static_cast<const BlockMatrix *>(c), &p, &meta);
   }
   return st == Status::kOk;
 }

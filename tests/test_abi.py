@@ -27,8 +27,9 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_cpp_api_symbols_exported():
-    """The C++ overload set of the reference (dsd.h, dds.h, sdd.h,
-    row_indices.h, transpose.h) with hipStream_t in place of cudaStream_t."""
+    """The C++ overload set of the reference (dsd.h, dds.h, sdd.h, ssd.h,
+    sds.h, row_indices.h, transpose.h) with hipStream_t in place of
+    cudaStream_t."""
     import subprocess
     out = subprocess.run(["nm", "-D", "--defined-only", sp.LIB_PATH],
                          capture_output=True, text=True, check=True).stdout
@@ -40,6 +41,11 @@ def test_cpp_api_symbols_exported():
         "_ZN7sputnik5block6MatmulENS0_6MatrixEbS1_bNS0_11BlockMatrixEP12ihipStream_t",
         "_ZN7sputnik5block10RowIndicesENS0_11BlockMatrixEPsP12ihipStream_t",
         "_ZN7sputnik5block9TransposeENS0_11BlockMatrixEP12ihipStream_t",
+        # SSD (ssd.h:10-22) and SDS (sds.h:10-22)
+        "_ZN7sputnik5block6MatmulENS0_11BlockMatrixEbNS0_6MatrixEbS1_P12ihipStream_t",
+        "_ZN7sputnik5block8MatmulExENS0_11BlockMatrixEbNS0_6MatrixEbS1_P12ihipStream_t",
+        "_ZN7sputnik5block6MatmulENS0_6MatrixEbNS0_11BlockMatrixEbS2_P12ihipStream_t",
+        "_ZN7sputnik5block8MatmulExENS0_6MatrixEbNS0_11BlockMatrixEbS2_P12ihipStream_t",
     ]
     for w in want:
         assert w in out, w

@@ -563,6 +563,99 @@ def test_tall_sparse_operand(op, ta, tb, dtype):
     H.assert_close(gpu, ref, dtype, f"tall {op}")
 
 
+# -------------------------------------------------------------- SSD / SDS --
+# The reference's problem lists (sputnik/block/ssd/ssd_test.cu:76-140 and
+# sds_test.cu:76-140), restated as data: (M, K, N, sparse-input blocks,
+# output blocks); each runs with all four transposes.
+_SS_SMALL = [(128, 128, 128, 1, 1), (128, 256, 128, 2, 1), (256, 128, 128, 2, 2),
+             (128, 128, 256, 1, 2), (128, 256, 128, 1, 1), (128, 128, 256, 1, 2),
+             (128, 256, 256, 1, 1), (256, 256, 256, 2, 2)]
+_SS_LARGE = [(512, 512, 1024, 16, 32), (512, 512, 1024, 8, 16),
+             (1024, 1024, 1024, 64, 64), (1024, 1024, 1024, 16, 16)]
+
+
+def _ss_params():
+    out = []
+    for m, k, n, nin, nout in _SS_SMALL + _SS_LARGE:
+        for ta in (False, True):
+            for tb in (False, True):
+                for unordered in ((False, True) if (m, k, n) == (256, 256, 256)
+                                  else (False,)):
+                    out.append(pytest.param(
+                        (m, k, n, nin, nout, ta, tb, unordered),
+                        id=f"m{m}k{k}n{n}-{nin}-{nout}-{'T' if ta else 'N'}"
+                           f"{'T' if tb else 'N'}{'-u' if unordered else ''}"))
+    return out
+
+
+def _blocks_at(ref_dense, Cs):
+    rows = np.repeat(np.arange(len(Cs.offsets) - 1), np.diff(Cs.offsets))
+    return np.stack([ref_dense[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128]
+                     for r, c in zip(rows, Cs.indices)])
+
+
+def _run_ss(op, case, dtype="f16", ex=False):
+    m, k, n, nin, nout, ta, tb, unordered = case
+    rng = np.random.default_rng(m * 31 + k * 7 + n + nin * 3 + nout)
+    # sparse-input capacity: A is M x K (SSD), B is K x N (SDS)
+    nin = min(nin, (m if op == "ssd" else n) // 128 * (k // 128))
+    Cs = H.HostSparse(m, n, nout * 16384, rng, dtype)
+    Cs.dev_values.fill_(float("nan"))
+    sp.AllocateRowIndicesBuffer(Cs.matrix)
+    sp.RowIndices(Cs.matrix, Cs.matrix.row_indices)
+    if op == "ssd":
+        A = H.HostSparse(*((k, m) if ta else (m, k)), nin * 16384, rng, dtype,
+                         unordered=unordered)
+        B = H.HostDense(*((n, k) if tb else (k, n)), rng, dtype)
+        sparse = A
+        ref = O.gemm(A.dense(), ta, B.values, tb, out_mask=Cs.mask(),
+                     threads=H.oracle_threads())
+        args = (A.matrix, ta, B.matrix, tb, Cs.matrix)
+    else:
+        A = H.HostDense(*((k, m) if ta else (m, k)), rng, dtype)
+        B = H.HostSparse(*((n, k) if tb else (k, n)), nin * 16384, rng, dtype,
+                         unordered=unordered)
+        sparse = B
+        ref = O.gemm(A.values, ta, B.dense(), tb, out_mask=Cs.mask(),
+                     threads=H.oracle_threads())
+        args = (A.matrix, ta, B.matrix, tb, Cs.matrix)
+    sp.AllocateTransposeBuffers(sparse.matrix)
+    if ex:
+        sp.Transpose(sparse.matrix)
+        sp.MatmulEx(*args)
+    else:
+        sp.Matmul(*args)
+    _sync()
+    return Cs.dev_values.float().cpu().numpy(), _blocks_at(ref, Cs)
+
+
+@pytest.mark.parametrize("case", _ss_params())
+def test_ssd_reference_problems(case):
+    """SSD: C_bcsr = op(A_bcsr) op(B) at C's blocks (reference ssd_test.cu),
+    fp16, against the oracle of the rounded inputs."""
+    gpu, ref = _run_ss("ssd", case)
+    H.assert_close(gpu, ref, "f16", "ssd")
+
+
+@pytest.mark.parametrize("case", _ss_params())
+def test_sds_reference_problems(case):
+    """SDS: C_bcsr = op(A) op(B_bcsr) at C's blocks (reference sds_test.cu)."""
+    gpu, ref = _run_ss("sds", case)
+    H.assert_close(gpu, ref, "f16", "sds")
+
+
+@pytest.mark.parametrize("op", ["ssd", "sds"])
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_ss_bf16_and_ex(op, ta, tb):
+    """bf16, and MatmulEx with precomputed transposed metadata."""
+    case = (512, 512, 1024, 8, 16, ta, tb, True)
+    gpu, ref = _run_ss(op, case, dtype="bf16")
+    H.assert_close(gpu, ref, "bf16", f"{op} bf16")
+    gpu, ref = _run_ss(op, case, ex=True)
+    H.assert_close(gpu, ref, "f16", f"{op} ex")
+
+
 # ------------------------------------------------------------ metadata ----
 
 def _device_topology(offsets, indices, rows_b, cols_b):
