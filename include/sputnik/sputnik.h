@@ -1,7 +1,6 @@
 // sputnik-amd umbrella header. Replaces reference sputnik/sputnik.h:18-25 for
-// the block-sparse products (DSD, DDS, SDD, SSD, SDS) and the metadata
-// builders (RowIndices, Transpose). DSS (sparse x sparse via bitmask
-// intersection) is not declared.
+// the six block-sparse products (DSD, DDS, SDD, SSD, SDS, DSS) and the
+// metadata builders (RowIndices, Transpose).
 #ifndef SPUTNIK_SPUTNIK_H_
 #define SPUTNIK_SPUTNIK_H_
 
@@ -11,6 +10,7 @@
 #include "sputnik/block/sdd/sdd.h"
 #include "sputnik/block/ssd/ssd.h"
 #include "sputnik/block/sds/sds.h"
+#include "sputnik/block/dss/dss.h"
 #include "sputnik/block/row_indices/row_indices.h"
 #include "sputnik/block/transpose/transpose.h"
 

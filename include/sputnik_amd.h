@@ -98,6 +98,16 @@ int sputnik_sds_ex(const sputnik_matrix_t *a, int transpose_a,
                    const sputnik_block_matrix_t *b, int transpose_b,
                    const sputnik_block_matrix_t *c, int dtype, void *stream);
 
+/* ---- DSS: C = op(A_bcsr) * op(B_bcsr), dense
+ *      (reference sputnik/block/dss/dss.h:10-22; K <= 32768; a's transposed
+ *      metadata when transpose_a, b's when !transpose_b; no bitmask needed) */
+int sputnik_dss(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream);
+int sputnik_dss_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream);
+
 /* ---- Metadata builders */
 /* reference sputnik/block/row_indices/row_indices.h:10 */
 int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,

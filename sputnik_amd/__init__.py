@@ -97,6 +97,8 @@ _SIGNATURES = {
     "sputnik_ssd_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_sds": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_sds_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dss": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dss_ex": [_P, ctypes.c_int, _P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_row_indices": [_P, _P, _P],
     "sputnik_transpose": [_P, _P],
     "sputnik_mask_to_bcsr": [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P],
@@ -252,17 +254,26 @@ def _call(ex: bool, a, transpose_a: bool, b, transpose_b: bool, c, stream):
                   _dtype_code(a.data), _stream(stream))
         _check(code, "sds")
         return
+    if (isinstance(a, BlockMatrix) and isinstance(b, BlockMatrix)
+            and isinstance(c, Matrix)):
+        ca, cb, cc = a._c(), b._c(), c._c()
+        fn = L.sputnik_dss_ex if ex else L.sputnik_dss
+        code = fn(ctypes.byref(ca), ta, ctypes.byref(cb), tb, ctypes.byref(cc),
+                  _dtype_code(c.data), _stream(stream))
+        _check(code, "dss")
+        return
     raise TypeError("no Matmul overload for these operand kinds")
 
 
 def Matmul(a, transpose_a, b, transpose_b, c, stream=None):  # noqa: N802
-    """DSD / DDS / SDD / SSD / SDS by operand kinds, like the C++ overload
-    set."""
+    """DSD / DDS / SDD / SSD / SDS / DSS by operand kinds, like the C++
+    overload set."""
     _call(False, a, transpose_a, b, transpose_b, c, stream)
 
 
 def MatmulEx(a, transpose_a, b, transpose_b, c, stream=None):  # noqa: N802
-    """DSD / DDS / SSD / SDS with the transposed metadata already present."""
+    """DSD / DDS / SSD / SDS / DSS with the transposed metadata already
+    present."""
     _call(True, a, transpose_a, b, transpose_b, c, stream)
 
 
@@ -327,7 +338,7 @@ def FreeRowIndicesBuffer(a: BlockMatrix):  # noqa: N802
     a.row_indices = None
 
 
-_OPS = {"dsd": 0, "dds": 1, "sdd": 2, "ssd": 3, "sds": 4}
+_OPS = {"dsd": 0, "dds": 1, "sdd": 2, "ssd": 3, "sds": 4, "dss": 5}
 
 
 def can_implement(op: str, a, transpose_a, b, transpose_b, c) -> bool:

@@ -37,10 +37,14 @@ hipError_t RunSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
                   const BlockMatrix &c, int dtype, bool build_meta,
                   hipStream_t stream, Status *status);
 
+hipError_t RunDss(const BlockMatrix &a, bool ta, const BlockMatrix &b,
+                  bool tb, const Matrix &c, int dtype, bool build_meta_a,
+                  bool build_meta_b, hipStream_t stream, Status *status);
+
 // hipError_t value the C-ABI returns for a status (never aborts).
 int StatusCode(Status st);
 
-// Host-only acceptance test. op 0 = DSD, 1 = DDS, 2 = SDD, 3 = SSD, 4 = SDS.
+// Host-only acceptance test. op 0 = DSD, 1 = DDS, 2 = SDD, 3 = SSD, 4 = SDS, 5 = DSS.
 bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
                   const void *c);
 

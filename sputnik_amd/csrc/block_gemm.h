@@ -134,6 +134,11 @@ struct GemmParams {
   unsigned *pair_flags;        // #pairs; 1 = partial published, reset to 0
                                // by the consumer (graph-replay safe)
   unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
+  // DSS (dense = sparse x sparse): op(B)'s column lists (k-block, storage
+  // block) — B's transposed metadata, or its own when op(B) = B^T.
+  const int *d_offsets;
+  const short *d_indices;
+  const int *d_block_offsets;  // nullptr: storage block = entry
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one
@@ -341,7 +346,7 @@ constexpr int kSpinLimit = 1 << 22;
 // kSKC / kDKC: S / D are k-contiguous in memory (else m/n-contiguous).
 // kOutT: write O transposed (DDS).
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
-          class Cfg, bool kSparseIn = false>
+          class Cfg, bool kSparseIn = false, bool kSparseD = false>
 __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                                   Cfg::kWGs * Cfg::kWM * Cfg::kWN / 4)
     block_gemm_kernel(const GemmParams p) {
@@ -377,6 +382,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr bool kDenseS = kSparseOut && !kSparseIn;  // SDD
   static_assert(!kSparseIn || (kSparseOut && !Cfg::kStagger && kBN == kBlock),
                 "SSD/SDS: one output block per workgroup, per-step pipeline");
+  // DSS: D is op(B)'s column block, one 128x128 output tile per workgroup;
+  // the k-list is the intersection of op(A)'s row and op(B)'s column.
+  static_assert(!kSparseD || (!kSparseOut && !kOutT && !Cfg::kStagger &&
+                              kBN == kBlock),
+                "DSS: dense 128x128 tiles, per-step pipeline");
+  constexpr int kDssMaxK = 256;  // k-blocks (K <= 32768, as the reference)
   constexpr int kIdxBytes =
       kDenseS ? (Cfg::kStagger ? 0 : 16)
                  : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
@@ -568,15 +579,26 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
                       : ge;
           }
           cached_e = e;
+        } else if constexpr (kSparseD) {
+          cached_e = e;
+          // intersection list staged by the DSS setup: S and D storage blocks
+          const int *ls = reinterpret_cast<const int *>(lds + kRingBytes) +
+                          kDssMaxK;
+          kblk = __builtin_amdgcn_readfirstlane(ls[kDssMaxK + e]);
+          blk = __builtin_amdgcn_readfirstlane(ls[e]);
         } else {
           cached_e = e;
           kblk = __builtin_amdgcn_readfirstlane((int)idx_kc[e]);
           blk = __builtin_amdgcn_readfirstlane(idx_blk[e]);
         }
         blk_s = p.s_data + (long long)blk * (kBlock * kBlock * 2);
-        const long long kg = (long long)kblk * kBlock;
-        blk_d = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
-                     : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+        if constexpr (kSparseD) {  // kblk holds D's storage block
+          blk_d = p.d_data + (long long)kblk * (kBlock * kBlock * 2);
+        } else {
+          const long long kg = (long long)kblk * kBlock;
+          blk_d = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
+                       : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+        }
       }
       s_base = blk_s + (kSKC ? h * (kBK * 2) : h * (kBK * 256));
       d_base = blk_d + (kDKC ? (long long)h * (kBK * 2)
@@ -1428,6 +1450,46 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if (kGrp > 2 && grp_count > 2) grp_c2 = p.c_indices[b0 + 2] * kBlock;
       if (kGrp > 3 && grp_count > 3) grp_c3 = p.c_indices[b0 + 3] * kBlock;
       __syncthreads();  // wsum / scratch reads done before the ring is used
+    } else if constexpr (kSparseD) {
+      // DSS tile (r, c): op(A)'s row r meets op(B)'s column c. LDS (after
+      // the ring): bmap[256] = D storage block of k-block k (or -1), then
+      // the intersection as S blocks [256] and D blocks [256], then count.
+      const int nc = p.num_jtiles;
+      srow = tile / nc;
+      const int c = tile % nc;
+      j0 = c * kBlock;
+      int *bmap = reinterpret_cast<int *>(lds + kRingBytes);
+      int *ls = bmap + kDssMaxK;
+      int *ld = ls + kDssMaxK;
+      int *cnt = ld + kDssMaxK;
+      for (int k = tid; k < kDssMaxK; k += kThreads) bmap[k] = -1;
+      __syncthreads();
+      const int b0 = p.d_offsets[c], b1 = p.d_offsets[c + 1];
+      for (int e = b0 + tid; e < b1; e += kThreads)
+        bmap[p.d_indices[e]] =
+            p.d_block_offsets != nullptr ? p.d_block_offsets[e] : e;
+      __syncthreads();
+      if (wave == 0) {  // order-preserving compaction of op(A)'s row
+        const int a0 = p.s_offsets[srow], a1 = p.s_offsets[srow + 1];
+        int pos = 0;
+        for (int base = a0; base < a1; base += 64) {
+          const int e = base + lane;
+          const bool valid = e < a1;
+          const int k = valid ? p.s_indices[e] : 0;
+          const int bm = valid ? bmap[k] : -1;
+          const bool hit = bm >= 0;
+          const unsigned long long ball = __ballot(hit);
+          if (hit) {
+            const int at = pos + __popcll(ball & ((1ull << lane) - 1));
+            ls[at] = p.s_block_offsets != nullptr ? p.s_block_offsets[e] : e;
+            ld[at] = bm;
+          }
+          pos += __popcll(ball);
+        }
+        if (lane == 0) cnt[0] = pos;
+      }
+      __syncthreads();
+      entries = __builtin_amdgcn_readfirstlane(cnt[0]);
     } else if constexpr (kSparseIn) {
       // SSD: block (r, c) of C is row r of op(A) times column panel c of
       // op(B). SDS computes the block transposed: row c of op(B)^T times
@@ -1508,6 +1570,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     exp_stamp(p.debug, 10, __builtin_amdgcn_s_memtime());
     if (do_collect) collect();
     exp_stamp(p.debug, 11, __builtin_amdgcn_s_memtime());
+  } else if constexpr (kSparseD) {
+    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
+    cached_e = -1;
+    pipeline(0, entries * kStepsPerBlock);  // list staged by the setup
   } else {
     exp_stamp(p.debug, 7, entries * kStepsPerBlock);
     run_sparse(entry0, 0, entries * kStepsPerBlock);
@@ -1544,6 +1610,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 hipError_t LaunchBlockGemm(int dtype, bool sparse_out, bool s_kc, bool d_kc,
                            bool out_t, bool grouped, const GemmParams &params,
                            hipStream_t stream);
+// DSS on CfgBlock: num_tiles = (M/128) x (N/128), num_jtiles = N/128.
+hipError_t LaunchBlockGemmDss(int dtype, bool s_kc, bool d_kc,
+                              const GemmParams &params, hipStream_t stream);
 // SSD (out_t = false) / SDS (out_t = true) on CfgBlock: num_tiles = C's
 // nonzero blocks.
 hipError_t LaunchBlockGemmSparseIn(int dtype, bool s_kc, bool d_kc, bool out_t,

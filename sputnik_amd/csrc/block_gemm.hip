@@ -84,7 +84,31 @@ hipError_t LaunchSparseIn(bool s_kc, bool d_kc, bool out_t,
 #undef SPUTNIK_SS
 }
 
+template <typename T>
+hipError_t LaunchDss(bool s_kc, bool d_kc, const GemmParams &p,
+                     hipStream_t stream) {
+  if (p.num_tiles <= 0) return hipSuccess;
+#define SPUTNIK_DSS(SKC, DKC)                                              \
+  hipLaunchKernelGGL(                                                      \
+      (block_gemm_kernel<T, false, SKC, DKC, false, CfgBlock, false,      \
+                         true>),                                           \
+      dim3(p.num_tiles), dim3(64 * CfgBlock::kWM * CfgBlock::kWN), 0,     \
+      stream, p);                                                          \
+  return hipGetLastError()
+  if (s_kc && !d_kc) { SPUTNIK_DSS(true, false); }    // DSS NN
+  if (s_kc && d_kc) { SPUTNIK_DSS(true, true); }      // DSS NT
+  if (!s_kc && !d_kc) { SPUTNIK_DSS(false, false); }  // DSS TN
+  SPUTNIK_DSS(false, true);                           // DSS TT
+#undef SPUTNIK_DSS
+}
+
 }  // namespace
+
+hipError_t LaunchBlockGemmDss(int dtype, bool s_kc, bool d_kc,
+                              const GemmParams &params, hipStream_t stream) {
+  if (dtype == 1) return LaunchDss<__bf16>(s_kc, d_kc, params, stream);
+  return LaunchDss<_Float16>(s_kc, d_kc, params, stream);
+}
 
 hipError_t LaunchBlockGemmSparseIn(int dtype, bool s_kc, bool d_kc, bool out_t,
                                    const GemmParams &params,

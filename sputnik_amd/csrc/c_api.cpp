@@ -161,6 +161,31 @@ int sputnik_sds_ex(const sputnik_matrix_t *a, int transpose_a,
                      stream);
 }
 
+static int DssEntry(bool ex, const sputnik_block_matrix_t *a, int ta,
+                    const sputnik_block_matrix_t *b, int tb,
+                    const sputnik_matrix_t *c, int dtype, void *stream) {
+  if (!a || !b || !c) return hipErrorInvalidValue;
+  BlockMatrix ca = ToCpp(a), cb = ToCpp(b);
+  if (ex) ca.create_metadata = cb.create_metadata = false;
+  sputnik_amd::Status st;
+  const hipError_t e = sputnik_amd::RunDss(
+      ca, ta != 0, cb, tb != 0, ToCpp(c), dtype, ca.create_metadata,
+      cb.create_metadata, static_cast<hipStream_t>(stream), &st);
+  return Code(e, sputnik_amd::StatusCode(st));
+}
+
+int sputnik_dss(const sputnik_block_matrix_t *a, int transpose_a,
+                const sputnik_block_matrix_t *b, int transpose_b,
+                const sputnik_matrix_t *c, int dtype, void *stream) {
+  return DssEntry(false, a, transpose_a, b, transpose_b, c, dtype, stream);
+}
+
+int sputnik_dss_ex(const sputnik_block_matrix_t *a, int transpose_a,
+                   const sputnik_block_matrix_t *b, int transpose_b,
+                   const sputnik_matrix_t *c, int dtype, void *stream) {
+  return DssEntry(true, a, transpose_a, b, transpose_b, c, dtype, stream);
+}
+
 int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
                         void *stream) {
   if (!a || (!row_indices && a->nonzeros > 0)) return hipErrorInvalidValue;

@@ -324,6 +324,50 @@ Status PrepareSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   return Status::kOk;
 }
 
+// DSS: C = op(A_bcsr) op(B_bcsr), dense (reference dss.cu:9-24). op(A)'s
+// rows use A's transposed metadata when transpose_a; op(B)'s columns use B's
+// transposed metadata unless transpose_b (dss_*_align8.cu). K <= 32768
+// (dss_nn:67). The reference's bitmask workspaces are not needed: the
+// intersection is built per tile in LDS.
+constexpr int kDssMaxK = 32768;
+Status PrepareDss(const BlockMatrix &a, bool ta, const BlockMatrix &b, bool tb,
+                  const Matrix &c, GemmParams *p, bool *meta_a,
+                  bool *meta_b) {
+  if (a.block_size != BlockSize::k128 || b.block_size != BlockSize::k128)
+    return Status::kNotSupported;
+  if (!SparseOk(a) || !SparseOk(b) || !DenseOk(c)) return Status::kNoKernel;
+  if (!ValidMatmul(a, ta, b, tb, c)) return Status::kNoKernel;
+  const MatmulShape s(a, ta, b, tb);
+  if (!Aligned8(s) || s.k > kDssMaxK) return Status::kNoKernel;
+  *meta_a = ta;
+  *meta_b = !tb;
+  if (ta && (a.offsets_t == nullptr || a.indices_t == nullptr ||
+             a.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+  if (!tb && (b.offsets_t == nullptr || b.indices_t == nullptr ||
+              b.block_offsets == nullptr))
+    return Status::kMissingMetadata;
+  *p = GemmParams{};
+  p->s_data = static_cast<const char *>(a.data);
+  p->s_offsets = static_cast<const int *>(ta ? a.offsets_t : a.offsets);
+  p->s_indices = static_cast<const short *>(ta ? a.indices_t : a.indices);
+  p->s_block_offsets =
+      ta ? static_cast<const int *>(a.block_offsets) : nullptr;
+  p->d_data = static_cast<const char *>(b.data);
+  p->d_ld = kBlock * 2;  // inside one stored 128x128 block
+  p->d_offsets = static_cast<const int *>(tb ? b.offsets : b.offsets_t);
+  p->d_indices = static_cast<const short *>(tb ? b.indices : b.indices_t);
+  p->d_block_offsets =
+      tb ? nullptr : static_cast<const int *>(b.block_offsets);
+  p->c_data = static_cast<char *>(c.data);
+  p->c_ld = (long long)s.ldc * 2;
+  p->num_rows = s.m / kBM;
+  p->num_jtiles = s.n / kBlock;
+  p->j_limit = s.n;
+  p->num_tiles = p->num_rows * p->num_jtiles;
+  return Status::kOk;
+}
+
 hipError_t BuildTransposed(const BlockMatrix &a, hipStream_t stream) {
   const int b = AsInt(a.block_size);
   if (b == 0) return hipErrorNotSupported;
@@ -497,6 +541,26 @@ hipError_t RunSds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
                                  /*out_t=*/true, p, stream);
 }
 
+hipError_t RunDss(const BlockMatrix &a, bool ta, const BlockMatrix &b,
+                  bool tb, const Matrix &c, int dtype, bool build_meta_a,
+                  bool build_meta_b, hipStream_t stream, Status *st_out) {
+  GemmParams p;
+  bool meta_a = false, meta_b = false;
+  const Status st = PrepareDss(a, ta, b, tb, c, &p, &meta_a, &meta_b);
+  *st_out = st;
+  if (st != Status::kOk) return hipSuccess;
+  if (meta_a && build_meta_a) {
+    const hipError_t e = BuildTransposed(a, stream);
+    if (e != hipSuccess) return e;
+  }
+  if (meta_b && build_meta_b) {
+    const hipError_t e = BuildTransposed(b, stream);
+    if (e != hipSuccess) return e;
+  }
+  p.debug = g_debug;
+  return LaunchBlockGemmDss(dtype, /*s_kc=*/!ta, /*d_kc=*/tb, p, stream);
+}
+
 }  // namespace sputnik_amd
 
 // ---- C++ API (drop-in for the reference's sputnik::block) ---------------
@@ -633,6 +697,36 @@ hipError_t MatmulEx(const Matrix a, bool transpose_a, const BlockMatrix b,
   return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
 }
 
+// DSS (reference sputnik/block/dss/dss.h:10-22).
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, Matrix c, DataType dtype,
+                  hipStream_t stream) {
+  Status st;
+  const hipError_t e = sputnik_amd::RunDss(
+      a, transpose_a, b, transpose_b, c, (int)dtype, a.create_metadata,
+      b.create_metadata, stream, &st);
+  return st == Status::kOk ? e : sputnik_amd::OrAbort(st, "dss");
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, Matrix c, DataType dtype,
+                    hipStream_t stream) {
+  BlockMatrix acp = a, bcp = b;
+  acp.create_metadata = false;
+  bcp.create_metadata = false;
+  return Matmul(acp, transpose_a, bcp, transpose_b, c, dtype, stream);
+}
+
+hipError_t Matmul(const BlockMatrix a, bool transpose_a, const BlockMatrix b,
+                  bool transpose_b, Matrix c, hipStream_t stream) {
+  return Matmul(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
+hipError_t MatmulEx(const BlockMatrix a, bool transpose_a, const BlockMatrix b,
+                    bool transpose_b, Matrix c, hipStream_t stream) {
+  return MatmulEx(a, transpose_a, b, transpose_b, c, DataType::kF16, stream);
+}
+
 hipError_t RowIndices(BlockMatrix a, short *row_indices, hipStream_t stream) {
   if (AsInt(a.block_size) == 0) return hipErrorNotSupported;
   return sputnik_amd::LaunchRowIndices(a.rows / AsInt(a.block_size),
@@ -660,7 +754,7 @@ int StatusCode(Status st) { return AsCode(st); }
 
 // Host-only acceptance test (no launch, no device needed): op 0 = DSD
 // (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block), 3 = SSD
-// (a, c: block), 4 = SDS (b, c: block). The C
+// (a, c: block), 4 = SDS (b, c: block), 5 = DSS (a, b: block). The C
 // descriptors share the C++ layout (static_asserts in c_api.cpp).
 bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
                   const void *c) {
@@ -688,6 +782,11 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
     st = PrepareSds(*static_cast<const Matrix *>(a), ta,
                     *static_cast<const BlockMatrix *>(b), tb,
                     *static_cast<const BlockMatrix *>(c), &p, &meta);
+  } else if (op == 5) {
+    bool meta_b = false;
+    st = PrepareDss(*static_cast<const BlockMatrix *>(a), ta,
+                    *static_cast<const BlockMatrix *>(b), tb,
+                    *static_cast<const Matrix *>(c), &p, &meta, &meta_b);
   }
   return st == Status::kOk;
 }

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_cpp_api_symbols_exported():
     """The C++ overload set of the reference (dsd.h, dds.h, sdd.h, ssd.h,
-    sds.h, row_indices.h, transpose.h) with hipStream_t in place of
+    sds.h, dss.h, row_indices.h, transpose.h) with hipStream_t in place of
     cudaStream_t."""
     import subprocess
     out = subprocess.run(["nm", "-D", "--defined-only", sp.LIB_PATH],
@@ -46,6 +46,9 @@ def test_cpp_api_symbols_exported():
         "_ZN7sputnik5block8MatmulExENS0_11BlockMatrixEbNS0_6MatrixEbS1_P12ihipStream_t",
         "_ZN7sputnik5block6MatmulENS0_6MatrixEbNS0_11BlockMatrixEbS2_P12ihipStream_t",
         "_ZN7sputnik5block8MatmulExENS0_6MatrixEbNS0_11BlockMatrixEbS2_P12ihipStream_t",
+        # DSS (dss.h:10-22)
+        "_ZN7sputnik5block6MatmulENS0_11BlockMatrixEbS1_bNS0_6MatrixEP12ihipStream_t",
+        "_ZN7sputnik5block8MatmulExENS0_11BlockMatrixEbS1_bNS0_6MatrixEP12ihipStream_t",
     ]
     for w in want:
         assert w in out, w

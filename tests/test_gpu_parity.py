@@ -656,6 +656,88 @@ def test_ss_bf16_and_ex(op, ta, tb):
     H.assert_close(gpu, ref, "f16", f"{op} ex")
 
 
+# -------------------------------------------------------------------- DSS --
+# The reference's problem list (sputnik/block/dss/dss_test.cu:78-140):
+# (M, K, N, A blocks, B blocks); small shapes with all four transposes, the
+# larger ones NN and NT as the reference runs them.
+_DSS_SMALL = [(128, 128, 128, 1, 1), (128, 256, 128, 2, 2), (256, 128, 128, 2, 1),
+              (128, 128, 256, 1, 2), (128, 256, 128, 1, 2), (128, 256, 128, 2, 1),
+              (128, 256, 128, 1, 1), (256, 128, 128, 1, 1), (128, 128, 256, 1, 1),
+              (256, 256, 256, 2, 2)]
+_DSS_LARGE = [(512, 512, 512, 16, 16), (512, 512, 512, 8, 8), (512, 512, 512, 4, 4),
+              (1024, 1024, 1024, 64, 64), (1024, 1024, 1024, 32, 32),
+              (1024, 1024, 1024, 16, 16)]
+
+
+def _dss_params():
+    out = []
+    for shape in _DSS_SMALL:
+        for ta in (False, True):
+            for tb in (False, True):
+                out.append((shape, ta, tb, shape == (256, 256, 256, 2, 2)))
+    for shape in _DSS_LARGE:
+        for tb in (False, True):
+            out.append((shape, False, tb, False))
+    return [pytest.param(p, id=f"m{p[0][0]}k{p[0][1]}n{p[0][2]}-{p[0][3]}-{p[0][4]}"
+                               f"-{'T' if p[1] else 'N'}{'T' if p[2] else 'N'}"
+                               f"{'-u' if p[3] else ''}") for p in out]
+
+
+def _run_dss(case, dtype="f16", ex=False):
+    (m, k, n, na, nb), ta, tb, unordered = case
+    rng = np.random.default_rng(m + 3 * k + 7 * n + 11 * na + 13 * nb)
+    A = H.HostSparse(*((k, m) if ta else (m, k)), na * 16384, rng, dtype,
+                     unordered=unordered)
+    B = H.HostSparse(*((n, k) if tb else (k, n)), nb * 16384, rng, dtype,
+                     unordered=unordered)
+    C, c_t = H.empty_dense(m, n, dtype)
+    sp.AllocateTransposeBuffers(A.matrix)
+    sp.AllocateTransposeBuffers(B.matrix)
+    if ex:
+        sp.Transpose(A.matrix)
+        sp.Transpose(B.matrix)
+        sp.MatmulEx(A.matrix, ta, B.matrix, tb, C)
+    else:
+        sp.Matmul(A.matrix, ta, B.matrix, tb, C)
+    _sync()
+    ref = O.gemm(A.dense(), ta, B.dense(), tb, threads=H.oracle_threads())
+    return c_t.float().cpu().numpy(), ref
+
+
+@pytest.mark.parametrize("case", _dss_params())
+def test_dss_reference_problems(case):
+    """DSS: dense C = op(A_bcsr) op(B_bcsr) (reference dss_test.cu), the
+    k-blocks of each output tile being the intersection of op(A)'s row and
+    op(B)'s column, against the oracle."""
+    gpu, ref = _run_dss(case)
+    H.assert_close(gpu, ref, "f16", "dss")
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_dss_bf16_ex_and_disjoint(ta, tb):
+    """bf16; MatmulEx with precomputed metadata; and operands whose patterns
+    never meet (every output tile empty: exact zeros)."""
+    case = ((512, 1024, 384, 12, 9), ta, tb, True)
+    gpu, ref = _run_dss(case, dtype="bf16")
+    H.assert_close(gpu, ref, "bf16", "dss bf16")
+    gpu, ref = _run_dss(case, ex=True)
+    H.assert_close(gpu, ref, "f16", "dss ex")
+    # A uses only k-blocks 0..3, B only 4..7: no intersection anywhere.
+    rng = np.random.default_rng(4)
+    a_off = np.array([0, 2, 4], np.int32)
+    a_idx = np.array([0, 3, 1, 2], np.int32)
+    b_off = np.array([0, 0, 0, 0, 0, 1, 2, 2, 3], np.int32)
+    b_idx = np.array([0, 1, 0], np.int32)
+    A = H.HostSparse(256, 1024, 4 * 16384, rng, topology=(a_off, a_idx))
+    B = H.HostSparse(1024, 256, 3 * 16384, rng, topology=(b_off, b_idx))
+    C, c_t = H.empty_dense(256, 256)
+    sp.AllocateTransposeBuffers(B.matrix)
+    sp.Matmul(A.matrix, False, B.matrix, False, C)
+    _sync()
+    assert int(torch.count_nonzero(c_t)) == 0
+
+
 # ------------------------------------------------------------ metadata ----
 
 def _device_topology(offsets, indices, rows_b, cols_b):
