@@ -443,11 +443,17 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
 // handles, so no LPT order and no pair balancing) have many more tiles than
 // CUs: they run on CfgTall, two workgroups per CU.
 bool UseTall(GemmParams *p) {
-  static const int disabled = [] {
+  // SPUTNIK_AMD_TALL: 0 never, 2 always (experiments), unset: tall only.
+  static const int mode = [] {
     const char *e = std::getenv("SPUTNIK_AMD_TALL");
-    return e != nullptr && std::atoi(e) == 0;
+    return e != nullptr ? std::atoi(e) : 1;
   }();
-  if (disabled || p->num_rows <= kLptRows || p->pair != 0) return false;
+  if (mode == 0) return false;
+  if (mode == 2) {
+    p->pair = 0;
+  } else if (p->num_rows <= kLptRows || p->pair != 0) {
+    return false;
+  }
   p->num_jtiles = (p->j_limit + CfgTall::kBN - 1) / CfgTall::kBN;
   p->num_tiles = p->num_rows * p->num_jtiles;
   return true;
