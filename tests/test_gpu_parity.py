@@ -157,7 +157,7 @@ def _skewed_topology(rows_b, cols_b, rng):
 
 
 @pytest.mark.parametrize("op", ["dsd", "dds"])
-@pytest.mark.parametrize("rows_b", [2, 7, 32])
+@pytest.mark.parametrize("rows_b", [2, 7, 32, 63, 100])
 def test_skewed_row_lengths(op, rows_b):
     """Skewed row lengths: DSD NN and DDS NT (row-order S) and their
     column-order variants, odd row counts, empty and full rows."""
