@@ -738,6 +738,42 @@ def test_dss_bf16_ex_and_disjoint(ta, tb):
     assert int(torch.count_nonzero(c_t)) == 0
 
 
+def test_more_than_65536_blocks():
+    """Block data beyond 2 GiB (71680 stored blocks: block index x 32 KiB
+    overflows int32, the reference's limit): DSD NN and TN
+    (transposed metadata, block_offsets > 65535) on a fully dense 128 x 560
+    block grid, sampled block-rows against the oracle."""
+    rows_b, cols_b, n = 128, 560, 64
+    nb = rows_b * cols_b
+    g = torch.Generator(device="cuda").manual_seed(65)
+    vals = (torch.rand(nb * 16384, generator=g, device="cuda") * 2 - 1).half()
+    off = np.arange(rows_b + 1, dtype=np.int32) * cols_b
+    idx = np.tile(np.arange(cols_b, dtype=np.int16), rows_b)
+    A = sp.BlockMatrix(rows_b * 128, cols_b * 128, 128, nb * 16384, vals,
+                       torch.from_numpy(off).cuda(), torch.from_numpy(idx).cuda())
+    rng = np.random.default_rng(66)
+    for ta in (False, True):
+        k = rows_b * 128 if ta else cols_b * 128
+        m = cols_b * 128 if ta else rows_b * 128
+        B = H.HostDense(k, n, rng)
+        C, c_t = H.empty_dense(m, n)
+        if ta:
+            sp.AllocateTransposeBuffers(A)
+        sp.Matmul(A, ta, B.matrix, False, C)
+        _sync()
+        for r in (0, m // 128 - 1, (m // 128) // 2):
+            if ta:   # row r of A^T = block-column r of A: blocks r, r+560, ...
+                blk = vals.view(nb, 128, 128)[r::cols_b].float().cpu().numpy()
+                a_rows = np.concatenate([b.T for b in blk], axis=1)  # 128 x k
+            else:    # block-row r: blocks r*560 .. +559
+                blk = vals.view(nb, 128, 128)[r * cols_b:(r + 1) * cols_b]
+                a_rows = blk.float().cpu().numpy().transpose(1, 0, 2).reshape(128, k)
+            ref = O.gemm(a_rows, False, B.values, False,
+                         threads=H.oracle_threads())
+            H.assert_close(c_t[r * 128:(r + 1) * 128].float().cpu().numpy(),
+                           ref, "f16", f"65536+ blocks ta={ta} row-block {r}")
+
+
 # ------------------------------------------------------------ metadata ----
 
 def _device_topology(offsets, indices, rows_b, cols_b):
