@@ -1343,7 +1343,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
     // Hand over only what exceeds the panel's balanced target, and nothing
     // under kMinHandoff blocks: a hand-off costs each side about one
     // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
-    constexpr int kMinHandoff = 2;
+#ifndef SPUTNIK_MIN_HANDOFF
+#define SPUTNIK_MIN_HANDOFF 2
+#endif
+    constexpr int kMinHandoff = SPUTNIK_MIN_HANDOFF;
     int hb = role == 1 ? 0 : n_h - pair_target;
     if (hb < kMinHandoff) hb = 0;
     pair_id = panel * half + pi;

@@ -64,11 +64,18 @@ static bool PairsEnabled() {
 
 // Fills the pair fields of p when pair balancing applies: a staggered
 // one-workgroup-per-CU tile config, every tile resident at once (the point
-// is the tail of a single wave of tiles) and rows rankable in-kernel.
-static void PreparePairs(GemmParams *p, hipStream_t stream) {
+// is the tail of a single wave of tiles) and rows rankable in-kernel. Below
+// a mean of 2 blocks per row the hand-offs cost more than the tail they
+// shorten (DSD 4096² at 5%: 23.7 µs with pairs, 20.3 µs without; unchanged
+// from 7% up, same-process A/B r01l).
+#ifndef SPUTNIK_PAIR_MIN_MEAN4
+#define SPUTNIK_PAIR_MIN_MEAN4 8  // 4 x mean blocks per row
+#endif
+static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair = 0;
   if (!CfgSparse::kStagger || CfgSparse::kWGs != 1) return;
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
+  if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
@@ -446,7 +453,10 @@ bool UseTall(GemmParams *p) {
   // SPUTNIK_AMD_TALL: 0 never, 2 always (experiments), unset: tall only.
   static const int mode = [] {
     const char *e = std::getenv("SPUTNIK_AMD_TALL");
-    return e != nullptr ? std::atoi(e) : 1;
+#ifndef SPUTNIK_TALL_MODE
+#define SPUTNIK_TALL_MODE 1
+#endif
+    return e != nullptr ? std::atoi(e) : SPUTNIK_TALL_MODE;
   }();
   if (mode == 0) return false;
   if (mode == 2) {
@@ -476,7 +486,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
-  PreparePairs(&p, stream);
+  PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
   const bool tall = UseTall(&p);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
@@ -494,7 +504,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
-  PreparePairs(&p, stream);
+  PreparePairs(&p, b.nonzeros / (kBlock * kBlock), stream);
   const bool tall = UseTall(&p);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);
