@@ -129,3 +129,48 @@ def slice_block_rows(offsets, indices, values, r0: int, r1: int):
     offsets = np.asarray(offsets)
     o0, o1 = int(offsets[r0]), int(offsets[r1])
     return (offsets[r0:r1 + 1] - o0).astype(np.int32), indices[o0:o1], values[o0:o1]
+
+
+def shard_cols_by_nnz(offsets: np.ndarray, indices: np.ndarray,
+                      block_cols: int, parts: int):
+    """DDS sharding: contiguous block-column panels of the sparse
+    operand B with balanced nonzero counts, [(c0, c1)] per part. The column
+    counts are offsets_t (transpose.cu:94-97), so this is shard_rows_by_nnz
+    over B's transposed row pointer; each rank computes C[:, c0·b : c1·b]
+    with A replicated."""
+    counts = np.bincount(np.asarray(indices, dtype=np.int64),
+                         minlength=block_cols)
+    offsets_t = np.concatenate([[0], np.cumsum(counts)])
+    return shard_rows_by_nnz(offsets_t, parts)
+
+
+def slice_block_cols(offsets, indices, values, c0: int, c1: int):
+    """Block-columns [c0, c1) of a BCSR matrix as a standalone BCSR matrix
+    (all block-rows, columns rebased to c0), with the matching block values.
+    Storage order is kept, so a row's blocks stay in their original order."""
+    offsets = np.asarray(offsets, dtype=np.int64)
+    idx = np.asarray(indices)
+    keep = (idx >= c0) & (idx < c1)
+    row_of = np.repeat(np.arange(len(offsets) - 1), np.diff(offsets))
+    per_row = np.bincount(row_of[keep], minlength=len(offsets) - 1)
+    p_off = np.concatenate([[0], np.cumsum(per_row)]).astype(np.int32)
+    return p_off, (idx[keep] - c0).astype(idx.dtype), values[keep]
+
+
+def shard_blocks(nb: int, parts: int):
+    """SDD sharding: the output's stored-block list split into
+    contiguous, equal runs [(b0, b1)] (the grid is over nb, so equal counts
+    are equal work). A and B are replicated."""
+    bounds = [nb * p // parts for p in range(parts + 1)]
+    return [(bounds[i], bounds[i + 1]) for i in range(parts)]
+
+
+def slice_blocks(offsets, indices, b0: int, b1: int):
+    """Stored blocks [b0, b1) of a BCSR output as a standalone BCSR topology
+    over the same block-rows (rows outside the run become empty). The rank's
+    `data` is the caller's data + b0·b² and its row_indices are
+    row_indices[b0:b1], so no block moves; the union over ranks writes every
+    stored block exactly once."""
+    offsets = np.asarray(offsets, dtype=np.int64)
+    p_off = (np.clip(offsets, b0, b1) - b0).astype(np.int32)
+    return p_off, np.asarray(indices)[b0:b1]

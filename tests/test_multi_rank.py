@@ -95,3 +95,113 @@ def test_two_rank_gloo_sharded_dsd_matches_unsharded(tmp_path):
     R, C, N, off, idx, vals, b = _problem()
     ref = O.gemm(mu.to_dense(R * 128, C * 128, off, idx, vals), False, b, False)
     assert np.array_equal(np.load(out), ref)
+
+
+# ---- DDS column panels and SDD block runs ----------------------
+
+def _pair_problem():
+    rng = np.random.default_rng(7)
+    M, KB, NB = 96, 5, 9           # A: M x K dense, B: K x N sparse (5 x 9 blocks)
+    off, idx = mu.random_topology(KB, NB, 20, rng, unordered=True)
+    vals = mu.random_values((20, 128, 128), rng)
+    a = mu.random_values((M, KB * 128), rng)
+    return M, KB, NB, off, idx, vals, a
+
+
+def _gather_equal(local, world):
+    t = torch.from_numpy(np.ascontiguousarray(local))
+    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([t.shape[0]]))
+    maxr = int(max(s.item() for s in sizes))
+    buf = torch.zeros((maxr,) + tuple(t.shape[1:]), dtype=t.dtype)
+    buf[: t.shape[0]] = t
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    return [bufs[i][: int(sizes[i].item())].numpy() for i in range(world)]
+
+
+def _worker_dds_sdd(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    M, KB, NB, off, idx, vals, a = _pair_problem()
+    # DDS: C[:, c0:c1] = A . B[:, c0:c1]; column panels balanced by nnz.
+    c0, c1 = mu.shard_cols_by_nnz(off, idx, NB, world)[rank]
+    p_off, p_idx, p_vals = mu.slice_block_cols(off, idx, vals, c0, c1)
+    cols = (c1 - c0) * 128
+    panel = np.zeros((cols, M), np.float32)   # gathered as C^T panels
+    if cols:
+        bd = mu.to_dense(KB * 128, cols, p_off, p_idx, p_vals)
+        panel = O.gemm(a, False, bd, False,
+                       b_mask=mu.block_mask(p_off, p_idx, c1 - c0)).T
+    dds = np.concatenate(_gather_equal(panel, world)).T
+    # SDD: C = x . w restricted to B's topology (KB x NB blocks), x = A^T
+    # (K x M), w (M x N); each rank computes the stored-block run [b0, b1).
+    nb = len(idx)
+    b0, b1 = mu.shard_blocks(nb, world)[rank]
+    s_off, s_idx = mu.slice_blocks(off, idx, b0, b1)
+    rows_of = np.repeat(np.arange(KB), np.diff(s_off))
+    x = a.T
+    w = mu.random_values((M, NB * 128), np.random.default_rng(11))
+    blocks = np.zeros((b1 - b0, 128, 128), np.float32)
+    for j in range(b1 - b0):
+        r, c = int(rows_of[j]), int(s_idx[j])
+        blocks[j] = O.gemm(x[r * 128:(r + 1) * 128], False,
+                           w[:, c * 128:(c + 1) * 128], False)
+    sdd = np.concatenate(_gather_equal(blocks, world))
+    if rank == 0:
+        np.savez(out_path, dds=dds, sdd=sdd)
+    dist.destroy_process_group()
+
+
+def test_shard_cols_and_blocks_cover_exactly_once():
+    rng = np.random.default_rng(3)
+    off, idx = mu.random_topology(16, 24, 150, rng, unordered=True)
+    counts = np.bincount(idx, minlength=24)
+    for parts in (1, 2, 3, 8):
+        sh = mu.shard_cols_by_nnz(off, idx, 24, parts)
+        assert sh[0][0] == 0 and sh[-1][1] == 24
+        assert all(p[1] == q[0] for p, q in zip(sh, sh[1:]))
+        loads = [counts[c0:c1].sum() for c0, c1 in sh]
+        assert sum(loads) == 150 and max(loads) - min(loads) <= 2 * counts.max()
+        vals = np.arange(150)
+        got = np.concatenate([mu.slice_block_cols(off, idx, vals, c0, c1)[2]
+                              for c0, c1 in sh])
+        assert sorted(got.tolist()) == list(range(150))
+        bl = mu.shard_blocks(150, parts)
+        assert bl[0][0] == 0 and bl[-1][1] == 150
+        assert max(b1 - b0 for b0, b1 in bl) - min(b1 - b0 for b0, b1 in bl) <= 1
+        ri = np.repeat(np.arange(16), np.diff(off))
+        for b0, b1 in bl:
+            s_off, s_idx = mu.slice_blocks(off, idx, b0, b1)
+            assert s_off[-1] == b1 - b0 and len(s_off) == 17
+            assert np.array_equal(np.repeat(np.arange(16), np.diff(s_off)),
+                                  ri[b0:b1])
+            assert np.array_equal(s_idx, idx[b0:b1])
+
+
+def test_slice_block_cols_matches_dense_columns():
+    rng = np.random.default_rng(4)
+    off, idx = mu.random_topology(4, 6, 11, rng, unordered=True)
+    vals = mu.random_values((11, 128, 128), rng)
+    dense = mu.to_dense(512, 768, off, idx, vals)
+    p_off, p_idx, p_vals = mu.slice_block_cols(off, idx, vals, 2, 5)
+    assert np.array_equal(mu.to_dense(512, 384, p_off, p_idx, p_vals),
+                          dense[:, 256:640])
+
+
+def test_two_rank_gloo_sharded_dds_and_sdd_match_unsharded(tmp_path):
+    from oracle import oracle as O
+    out = str(tmp_path / "c.npz")
+    mp.spawn(_worker_dds_sdd, args=(2, _free_port(), out), nprocs=2, join=True)
+    M, KB, NB, off, idx, vals, a = _pair_problem()
+    got = np.load(out)
+    ref = O.gemm(a, False, mu.to_dense(KB * 128, NB * 128, off, idx, vals), False)
+    assert np.array_equal(got["dds"], ref)
+    w = mu.random_values((M, NB * 128), np.random.default_rng(11))
+    full = O.gemm(a.T, False, w, False)
+    ri = np.repeat(np.arange(KB), np.diff(off))
+    want = np.stack([full[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128]
+                     for r, c in zip(ri, idx)])
+    assert np.array_equal(got["sdd"], want)
