@@ -278,10 +278,15 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
 // sets the register budget through __launch_bounds__ and must match the LDS
 // footprint).
 template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_,
-          int STAGGER_ = 0>
+          int STAGGER_ = 0, int KSPLIT_ = 1>
 struct TileConfig {
   static constexpr int kBN = BN_, kWM = WM_, kWN = WN_, kBK = BK_;
   static constexpr int kStages = STAGES_, kWGs = WGS_;
+  // kKSplit = 2: two wave sets own the same kWM x kWN sub-tiles and split
+  // each slot's k depth between them (set h takes k-half h); their fp32
+  // accumulators are summed through LDS before the epilogue.
+  static constexpr int kKSplit = KSPLIT_;
+  static constexpr int kWaves = WM_ * WN_ * KSPLIT_;
   // kStagger: the two halves of the waves (wave w and w + kNW/2 share a
   // SIMD) run one barrier apart, so one half's DMA/read phase overlaps the
   // other half's MFMA phase (needs kStages >= 4; see the pipeline).
@@ -309,6 +314,10 @@ using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
+// SDD, one block per workgroup with K split inside it: 8 waves in two
+// staggered halves, each half a 2x2 set of 64x64 sub-tiles over its k-half of
+// a 64-deep slot (two waves per SIMD where CfgBlock has one).
+using CfgBlockKS = TileConfig<128, 2, 2, 64, 4, 1, 1, 2>;
 // SDD, grouped: up to 4 consecutive stored blocks of one block-row per
 // workgroup (shared S rows, D columns gathered per lane), on the staggered
 // 128x512 pipeline of CfgWide8S.
@@ -328,8 +337,11 @@ using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
 #define SPUTNIK_TALL_CFG CfgDual
 #endif
 using CfgTall = SPUTNIK_TALL_CFG;
+// k-split SDD (CfgBlockKS) vs CfgBlock, DSD-shaped 4096^3, interleaved A/B
+// (scripts/exp_ks*.sh): 20% 54.9 -> 33.2 us, 50% 114.9 -> 74.8 us, 90%
+// 216.6 -> 147.9 us, parity green on every reference SDD problem.
 #ifndef SPUTNIK_SDD_CFG
-#define SPUTNIK_SDD_CFG CfgBlock
+#define SPUTNIK_SDD_CFG CfgBlockKS
 #endif
 using CfgSdd = SPUTNIK_SDD_CFG;        // SDD tile configuration (BN = 128)
 
@@ -347,19 +359,20 @@ constexpr int kSpinLimit = 1 << 22;
 // kOutT: write O transposed (DDS).
 template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
           class Cfg, bool kSparseIn = false, bool kSparseD = false>
-__global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
-                                  Cfg::kWGs * Cfg::kWM * Cfg::kWN / 4)
+__global__ void __launch_bounds__(64 * Cfg::kWaves,
+                                  Cfg::kWGs * Cfg::kWaves / 4)
     block_gemm_kernel(const GemmParams p) {
   constexpr int kBN = Cfg::kBN;
   constexpr int kBK = Cfg::kBK;
   constexpr int kStages = Cfg::kStages;
   constexpr int kWN = Cfg::kWN;
-  constexpr int kNW = Cfg::kWM * Cfg::kWN;   // waves per workgroup
+  constexpr int kNW = Cfg::kWaves;           // waves per workgroup
+  constexpr int kKS = Cfg::kKSplit;
   constexpr int kTM = kBM / Cfg::kWM;        // wave sub-tile rows
   constexpr int kTN = kBN / Cfg::kWN;        // wave sub-tile cols
   constexpr int kFM = kTM / 16;              // 16x16 accumulators per wave
   constexpr int kFN = kTN / 16;
-  constexpr int kKK = kBK / 32;              // MFMA k-steps per slot
+  constexpr int kKK = kBK / 32 / kKS;        // MFMA k-steps per slot and wave
   constexpr int kThreads = 64 * kNW;
   constexpr int kSBytes = kBM * kBK * 2;
   constexpr int kDBytes = kBK * kBN * 2;
@@ -396,7 +409,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   constexpr bool kGroupedSdd = kDenseS && kBN > kBlock;
   constexpr int kGrp = kBN / kBlock;
   static_assert(!Cfg::kStagger || kStages >= 4, "stagger needs 4 slots");
-  static_assert(!Cfg::kStagger || (Cfg::kWM * Cfg::kWN) % 2 == 0, "halves");
+  static_assert(!Cfg::kStagger || kNW % 2 == 0, "halves");
+  static_assert(kKS == 1 || (kKS == 2 && Cfg::kStagger && kDenseS &&
+                             !kGroupedSdd && kKK >= 1),
+                "k split: staggered single-block SDD only");
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
   static_assert(kTM % 16 == 0 && kTN % 16 == 0 && kBK % 32 == 0, "tiles");
@@ -415,8 +431,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / kWN;
-  const int wn = wave % kWN;
+  const int wsub = kKS > 1 ? wave % (Cfg::kWM * kWN) : wave;
+  const int wm = wsub / kWN;
+  const int wn = wsub % kWN;
+  // k split: this wave's first 32-deep k-step inside a slot.
+  const int kk0 = kKS > 1 ? (wave / (Cfg::kWM * kWN)) * kKK : 0;
   const int row_w = kTM * wm;  // first row / col of this wave's sub-tile
   const int col_w = kTN * wn;
 
@@ -649,16 +668,16 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
 #pragma unroll
       for (int f = 0; f < kFM; ++f) {
         if constexpr (kSKC)
-          F.a[kk][f] = read_kc<kKcRow>(simg, row_w + 16 * f, kk, lane);
+          F.a[kk][f] = read_kc<kKcRow>(simg, row_w + 16 * f, kk0 + kk, lane);
         else
-          F.a[kk][f] = read_mn<kBM * 2>(simg, row_w + 16 * f, kk, lane);
+          F.a[kk][f] = read_mn<kBM * 2>(simg, row_w + 16 * f, kk0 + kk, lane);
       }
 #pragma unroll
       for (int f = 0; f < kFN; ++f) {
         if constexpr (kDKC)
-          F.b[kk][f] = read_kc<kKcRow>(dimg, col_w + 16 * f, kk, lane);
+          F.b[kk][f] = read_kc<kKcRow>(dimg, col_w + 16 * f, kk0 + kk, lane);
         else
-          F.b[kk][f] = read_mn<kDRowBytes>(dimg, col_w + 16 * f, kk, lane);
+          F.b[kk][f] = read_mn<kDRowBytes>(dimg, col_w + 16 * f, kk0 + kk, lane);
       }
     }
   };
@@ -1121,6 +1140,30 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
   auto write_tile = [&](long long out_block) {
     wait_vmcnt<0>();
     __syncthreads();
+    if constexpr (kKS > 1) {
+      // Sum the two k-halves: the second wave set parks its fp32
+      // accumulators in the upper half of the ring (the staging image below
+      // stays under it), the first adds them and stages the tile.
+      static_assert(kBM * (kBN * 2 + 16) <= kRingBytes / 2 &&
+                        kNW / 2 * kFM * kFN * 1024 <= kRingBytes / 2,
+                    "k-split exchange fits beside the staging image");
+      f32x4 *xch = reinterpret_cast<f32x4 *>(lds + kRingBytes / 2) +
+                   wsub * (kFM * kFN * 64) + lane;
+      const bool second = wave >= kNW / 2;
+      if (second) {
+#pragma unroll
+        for (int a = 0; a < kFM; ++a)
+#pragma unroll
+          for (int b = 0; b < kFN; ++b) xch[(a * kFN + b) * 64] = acc[a][b];
+      }
+      __syncthreads();
+      if (!second) {
+#pragma unroll
+        for (int a = 0; a < kFM; ++a)
+#pragma unroll
+          for (int b = 0; b < kFN; ++b) acc[a][b] += xch[(a * kFN + b) * 64];
+      }
+    }
     constexpr int kStLdNT = kBN * 2 + 16;  // straight staging row
     constexpr int kStLdT = kBM * 2 + 16;   // transposed staging row
     constexpr int kPasses =
@@ -1139,6 +1182,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWM * Cfg::kWN,
       if (pass > 0) __syncthreads();  // previous slice fully stored
 #pragma unroll
       for (int a = 0; a < kFM; ++a) {
+        if (kKS > 1 && wave >= kNW / 2) break;  // k split: first set stages
 #pragma unroll
         for (int b = 0; b < kFN; ++b) {
           const int jb = col_w + 16 * b;  // wave-uniform

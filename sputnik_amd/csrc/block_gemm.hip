@@ -14,7 +14,7 @@ template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
           class Cfg>
 hipError_t LaunchCfg(const GemmParams &p, hipStream_t stream) {
   hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, Cfg>),
-                     dim3(p.num_tiles), dim3(64 * Cfg::kWM * Cfg::kWN), 0,
+                     dim3(p.num_tiles), dim3(64 * Cfg::kWaves), 0,
                      stream, p);
   return hipGetLastError();
 }
@@ -68,7 +68,7 @@ hipError_t LaunchSparseIn(bool s_kc, bool d_kc, bool out_t,
 #define SPUTNIK_SS(SKC, DKC, OUTT)                                         \
   hipLaunchKernelGGL(                                                      \
       (block_gemm_kernel<T, true, SKC, DKC, OUTT, CfgBlock, true>),       \
-      dim3(p.num_tiles), dim3(64 * CfgBlock::kWM * CfgBlock::kWN), 0,     \
+      dim3(p.num_tiles), dim3(64 * CfgBlock::kWaves), 0,     \
       stream, p);                                                          \
   return hipGetLastError()
   switch (code) {
@@ -92,7 +92,7 @@ hipError_t LaunchDss(bool s_kc, bool d_kc, const GemmParams &p,
   hipLaunchKernelGGL(                                                      \
       (block_gemm_kernel<T, false, SKC, DKC, false, CfgBlock, false,      \
                          true>),                                           \
-      dim3(p.num_tiles), dim3(64 * CfgBlock::kWM * CfgBlock::kWN), 0,     \
+      dim3(p.num_tiles), dim3(64 * CfgBlock::kWaves), 0,     \
       stream, p);                                                          \
   return hipGetLastError()
   if (s_kc && !d_kc) { SPUTNIK_DSS(true, false); }    // DSS NN
