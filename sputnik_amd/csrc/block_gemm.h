@@ -344,6 +344,17 @@ using CfgTall = SPUTNIK_TALL_CFG;
 #define SPUTNIK_SDD_CFG CfgBlockKS
 #endif
 using CfgSdd = SPUTNIK_SDD_CFG;        // SDD tile configuration (BN = 128)
+// The same k split on SSD / SDS / DSS, 4096^3 fp16 (sparse inputs 50%, sparse
+// output 20%; scripts/exp_ksall.sh): SSD 37.3 -> 29.9 us, SDS 35.3 -> 29.1 us,
+// DSS NT 86.6 -> 62.4 us, parity green on all their reference problems.
+#ifndef SPUTNIK_SS_CFG
+#define SPUTNIK_SS_CFG CfgBlockKS
+#endif
+using CfgSs = SPUTNIK_SS_CFG;          // SSD / SDS tile configuration
+#ifndef SPUTNIK_DSS_CFG
+#define SPUTNIK_DSS_CFG CfgBlockKS
+#endif
+using CfgDss = SPUTNIK_DSS_CFG;        // DSS tile configuration
 
 // Bounded spin for the pair hand-off (about 0.1 s): a launch can never hang
 // on a missing partial. The producer never waits and always has a lower
@@ -390,14 +401,17 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr int kRingBytes = kStages * kStageBytes;
   // Index list staged per chunk in LDS (smaller when three workgroups share
   // a CU); staggered configs read it with scalar loads instead.
-  constexpr bool kScalarIdx = Cfg::kStagger;
+  constexpr bool kScalarIdx = Cfg::kStagger && !kSparseIn && !kSparseD;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
   constexpr bool kDenseS = kSparseOut && !kSparseIn;  // SDD
-  static_assert(!kSparseIn || (kSparseOut && !Cfg::kStagger && kBN == kBlock),
+  static_assert(!kSparseIn || (kSparseOut &&
+                               (!Cfg::kStagger || Cfg::kKSplit == 2) &&
+                               kBN == kBlock),
                 "SSD/SDS: one output block per workgroup, per-step pipeline");
   // DSS: D is op(B)'s column block, one 128x128 output tile per workgroup;
   // the k-list is the intersection of op(A)'s row and op(B)'s column.
-  static_assert(!kSparseD || (!kSparseOut && !kOutT && !Cfg::kStagger &&
+  static_assert(!kSparseD || (!kSparseOut && !kOutT &&
+                              (!Cfg::kStagger || Cfg::kKSplit == 2) &&
                               kBN == kBlock),
                 "DSS: dense 128x128 tiles, per-step pipeline");
   constexpr int kDssMaxK = 256;  // k-blocks (K <= 32768, as the reference)
@@ -410,9 +424,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr int kGrp = kBN / kBlock;
   static_assert(!Cfg::kStagger || kStages >= 4, "stagger needs 4 slots");
   static_assert(!Cfg::kStagger || kNW % 2 == 0, "halves");
-  static_assert(kKS == 1 || (kKS == 2 && Cfg::kStagger && kDenseS &&
+  static_assert(kKS == 1 || (kKS == 2 && Cfg::kStagger && kBN == kBlock &&
                              !kGroupedSdd && kKK >= 1),
-                "k split: staggered single-block SDD only");
+                "k split: staggered single-block tiles only");
   static_assert(kSInstr * kNW * 1024 == kSBytes, "S DMA split");
   static_assert(kDInstr * kNW * 1024 == kDBytes, "D DMA split");
   static_assert(kTM % 16 == 0 && kTN % 16 == 0 && kBK % 32 == 0, "tiles");

@@ -67,8 +67,8 @@ hipError_t LaunchSparseIn(bool s_kc, bool d_kc, bool out_t,
   const int code = (s_kc ? 4 : 0) | (d_kc ? 2 : 0) | (out_t ? 1 : 0);
 #define SPUTNIK_SS(SKC, DKC, OUTT)                                         \
   hipLaunchKernelGGL(                                                      \
-      (block_gemm_kernel<T, true, SKC, DKC, OUTT, CfgBlock, true>),       \
-      dim3(p.num_tiles), dim3(64 * CfgBlock::kWaves), 0,     \
+      (block_gemm_kernel<T, true, SKC, DKC, OUTT, CfgSs, true>),       \
+      dim3(p.num_tiles), dim3(64 * CfgSs::kWaves), 0,          \
       stream, p);                                                          \
   return hipGetLastError()
   switch (code) {
@@ -90,9 +90,9 @@ hipError_t LaunchDss(bool s_kc, bool d_kc, const GemmParams &p,
   if (p.num_tiles <= 0) return hipSuccess;
 #define SPUTNIK_DSS(SKC, DKC)                                              \
   hipLaunchKernelGGL(                                                      \
-      (block_gemm_kernel<T, false, SKC, DKC, false, CfgBlock, false,      \
+      (block_gemm_kernel<T, false, SKC, DKC, false, CfgDss, false,      \
                          true>),                                           \
-      dim3(p.num_tiles), dim3(64 * CfgBlock::kWaves), 0,     \
+      dim3(p.num_tiles), dim3(64 * CfgDss::kWaves), 0,     \
       stream, p);                                                          \
   return hipGetLastError()
   if (s_kc && !d_kc) { SPUTNIK_DSS(true, false); }    // DSS NN
