@@ -435,7 +435,13 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
                             dev) != hipSuccess)
     return false;
-  if (blocks < kGrp * cus || p->num_rows > kMaxGroupRows) return false;
+  // Below ~6 blocks per CU the k-split block tile is faster (SDD 8192^2 x
+  // 8192, scripts/exp_grp.sh: 4 per CU 320 vs 367 us grouped; 8 per CU
+  // 656 vs 577 us).
+  constexpr int kGroupedMinPerCu = 6;
+  static_assert(kGroupedMinPerCu >= kGrp, "a grouped grid fills every CU");
+  if (blocks < kGroupedMinPerCu * cus || p->num_rows > kMaxGroupRows)
+    return false;
   // D lane offsets: k-contiguous D gathers whole rows (n * ldb); otherwise
   // one 32-row k panel plus any column.
   const long long span = d_kc ? (long long)p->j_limit * p->d_ld
