@@ -40,7 +40,7 @@ typedef struct sputnik_block_matrix {
   void *indices_t;     /* int16[#blocks] */
   void *block_offsets; /* int32[#blocks] */
   void *row_indices;   /* int16[#blocks] */
-  void *bitmask;       /* unused by this library */
+  void *bitmask;       /* uint64 BitMatrix words (sputnik_bitmask) */
   uint8_t create_metadata; /* C++ bool */
 } sputnik_block_matrix_t;
 
@@ -115,6 +115,14 @@ int sputnik_row_indices(const sputnik_block_matrix_t *a, int16_t *row_indices,
 /* reference sputnik/block/transpose/transpose.h:10 (device, bit-identical) */
 int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream);
 
+/* reference sputnik/block/bitmask/bitmask.h:10 (device, bit-identical
+ * BitMatrix layout: rows of ceil(cols/64) uint64 words). Orientation as the
+ * reference: over the transposed order when m->offsets_t is set. */
+int sputnik_bitmask(const sputnik_block_matrix_t *m, void *stream);
+/* Bytes of m's bitmask workspace (reference AllocateBitmaskBuffers,
+ * bitmask.h:16-23; host-only). */
+size_t sputnik_bitmask_bytes(const sputnik_block_matrix_t *m);
+
 /* ---- Device topology builders (no host round trip) */
 /* Block mask (uint8 [block_rows][block_cols] row-major, nonzero = present)
  * -> BCSR offsets int32[block_rows+1] and ascending int16 indices, the
@@ -142,6 +150,23 @@ size_t sputnik_abi_block_matrix_size(void);
 size_t sputnik_abi_block_matrix_offset(int field);
 size_t sputnik_abi_matrix_size(void);
 const char *sputnik_version(void);
+/* Hash of the sources the library was built from (bench.py compares it
+ * with the tree it runs in). */
+const char *sputnik_build_hash(void);
+
+/* ---- Diagnostics (need a device) */
+/* SDD tile plan: 1 = grouped 128x512 tiles (>= 6 blocks per CU), 0 = one
+ * k-split 128x128 block per workgroup, -1 = the problem is rejected. */
+int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
+                     const sputnik_matrix_t *b, int transpose_b,
+                     const sputnik_block_matrix_t *c);
+/* Number of pair-balancing workspaces of the current device in which a
+ * consumer workgroup timed out waiting for its partial since the last call
+ * (its output tile was written as NaN); clears them. Synchronizes. -1 on a
+ * HIP error. */
+int sputnik_pair_errors(void);
+/* Test knob: when on, pair producers never publish (forces the timeout). */
+void sputnik_debug_pair_fault(int on);
 
 #ifdef __cplusplus
 }  /* extern "C" */

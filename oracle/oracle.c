@@ -83,6 +83,22 @@ void oracle_transpose(int block_rows, int block_cols, const int32_t *offsets,
   free(cursor);
 }
 
+/* Block bit matrix. sputnik/block/bitmask/bitmask.cu:31-39 over the layout
+ * of bit_matrix.h:14-40: rows of ceil(cols / 64) uint64 words (kAlignment =
+ * 64), bit j % 64 of word i * words + j / 64 set for every stored block
+ * (i, j). The caller passes the metadata of the wanted orientation
+ * (bitmask.cu:8-16: offsets_t / indices_t when the transposed one is set). */
+void oracle_bitmask(int block_rows, int block_cols, const int32_t *offsets,
+                    const int16_t *indices, uint64_t *words_out) {
+  const int64_t words = (block_cols + 63) / 64;
+  memset(words_out, 0, sizeof(uint64_t) * (size_t)(words * block_rows));
+  for (int i = 0; i < block_rows; ++i)
+    for (int off = offsets[i]; off < offsets[i + 1]; ++off) {
+      const int j = indices[off];
+      words_out[i * words + j / 64] |= 1ull << (j % 64);
+    }
+}
+
 /* BCSR -> dense row-major. sputnik/block/matrix_utils.h:81-112 (ToMatrix):
  * block l of block-row i lands at rows i*bd.., cols indices[l]*bd.., values
  * read row-major from values + l*bd*bd. */

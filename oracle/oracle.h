@@ -15,6 +15,8 @@ void oracle_row_indices(int block_rows, const int32_t *offsets,
 void oracle_transpose(int block_rows, int block_cols, const int32_t *offsets,
                       const int16_t *indices, int32_t *offsets_t,
                       int16_t *indices_t, int32_t *block_offsets);
+void oracle_bitmask(int block_rows, int block_cols, const int32_t *offsets,
+                    const int16_t *indices, uint64_t *words_out);
 void oracle_bcsr_to_dense(int rows, int cols, int bd, const int32_t *offsets,
                           const int16_t *indices, const float *values,
                           float *out);

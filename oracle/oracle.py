@@ -39,6 +39,8 @@ def lib():
         L.oracle_row_indices.restype = None
         L.oracle_transpose.argtypes = [I, I, P, P, P, P, P]
         L.oracle_transpose.restype = None
+        L.oracle_bitmask.argtypes = [I, I, P, P, P]
+        L.oracle_bitmask.restype = None
         L.oracle_bcsr_to_dense.argtypes = [I, I, I, P, P, P, P]
         L.oracle_bcsr_to_dense.restype = None
         L.oracle_gemm.argtypes = [I, I, I, P, I, P, I, P, P, P, P, I]
@@ -83,6 +85,17 @@ def transpose(offsets: np.ndarray, indices: np.ndarray, block_cols: int):
                            _p(indices), _p(offsets_t), _p(indices_t),
                            _p(block_offsets))
     return offsets_t, indices_t[:nb], block_offsets[:nb]
+
+
+def bitmask(offsets: np.ndarray, indices: np.ndarray, block_cols: int):
+    """-> uint64 [block_rows, ceil(block_cols/64)] (bitmask.cu:31-39)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.int32)
+    indices = np.ascontiguousarray(indices, dtype=np.int16)
+    rows = len(offsets) - 1
+    words = (block_cols + 63) // 64
+    out = np.zeros((max(rows, 1), max(words, 1)), dtype=np.uint64)
+    lib().oracle_bitmask(rows, block_cols, _p(offsets), _p(indices), _p(out))
+    return out[:rows, :words]
 
 
 def bcsr_to_dense(rows, cols, offsets, indices, values, block=128):

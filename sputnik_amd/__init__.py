@@ -109,12 +109,21 @@ _SIGNATURES = {
     "sputnik_abi_block_matrix_offset": [ctypes.c_int],
     "sputnik_abi_matrix_size": [],
     "sputnik_version": [],
+    "sputnik_build_hash": [],
+    "sputnik_bitmask": [_P, _P],
+    "sputnik_bitmask_bytes": [_P],
+    "sputnik_sdd_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_pair_errors": [],
+    "sputnik_debug_pair_fault": [ctypes.c_int],
 }
 _RESTYPES = {
     "sputnik_abi_block_matrix_size": ctypes.c_size_t,
     "sputnik_abi_block_matrix_offset": ctypes.c_size_t,
     "sputnik_abi_matrix_size": ctypes.c_size_t,
     "sputnik_version": ctypes.c_char_p,
+    "sputnik_build_hash": ctypes.c_char_p,
+    "sputnik_bitmask_bytes": ctypes.c_size_t,
+    "sputnik_debug_pair_fault": None,
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -311,6 +320,46 @@ def ExpertTopology(padded_bins, block_rows, blocks_per_expert, offsets,  # noqa:
         _stream(stream)), "ExpertTopology")
 
 
+def Bitmask(m: BlockMatrix, stream=None):  # noqa: N802
+    """reference sputnik/block/bitmask/bitmask.h:10 (on the device): the
+    BitMatrix of m's topology, over the transposed order when m.offsets_t is
+    set (call AllocateBitmaskBuffers after AllocateTransposeBuffers then)."""
+    cm = m._c()
+    _check(lib().sputnik_bitmask(ctypes.byref(cm), _stream(stream)), "Bitmask")
+
+
+def AllocateBitmaskBuffers(m: BlockMatrix):  # noqa: N802
+    """reference bitmask.h:16-23 (uint64 words, torch-owned)."""
+    import torch
+
+    cm = m._c()
+    words = lib().sputnik_bitmask_bytes(ctypes.byref(cm)) // 8
+    m.bitmask = torch.empty(max(int(words), 1), dtype=torch.int64,
+                            device=m.offsets.device)
+
+
+def FreeBitmaskBuffers(m: BlockMatrix):  # noqa: N802
+    m.bitmask = None
+
+
+def sdd_plan(a, transpose_a, b, transpose_b, c) -> int:
+    """SDD tile plan the dispatcher picks on the current device: 1 grouped
+    128x512 tiles, 0 one k-split block per workgroup, -1 rejected."""
+    ca, cb, cc = a._c(), b._c(), c._c()
+    return int(lib().sputnik_sdd_plan(ctypes.byref(ca), int(bool(transpose_a)),
+                                      ctypes.byref(cb), int(bool(transpose_b)),
+                                      ctypes.byref(cc)))
+
+
+def pair_errors() -> int:
+    """Timed-out pair hand-offs since the last call (their tiles are NaN)."""
+    return int(lib().sputnik_pair_errors())
+
+
+def build_hash() -> str:
+    return lib().sputnik_build_hash().decode()
+
+
 def AllocateTransposeBuffers(a: BlockMatrix):  # noqa: N802
     """reference arguments.h:233-245 (torch-owned device workspaces)."""
     import torch
@@ -354,7 +403,9 @@ def version() -> str:
 
 
 __all__ = [
-    "AllocateRowIndicesBuffer", "AllocateTransposeBuffers", "AsInt",
+    "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
+    "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
+    "build_hash", "pair_errors", "sdd_plan",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",

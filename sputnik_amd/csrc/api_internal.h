@@ -48,6 +48,16 @@ int StatusCode(Status st);
 bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
                   const void *c);
 
+// SDD tile plan of a valid problem: 1 = grouped 128x512 tiles, 0 = one
+// k-split 128x128 block per workgroup, -1 = rejected. Reads the CU count of
+// the current device (no launch).
+int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
+
+// Pair hand-offs that timed out (see dispatch.cpp), and the test knob that
+// makes every pair producer skip its publish.
+int PairErrors();
+void SetPairFault(int on);
+
 }  // namespace sputnik_amd
 
 #endif  // SPUTNIK_AMD_API_INTERNAL_H_

@@ -47,7 +47,6 @@
 // the shipped library is built with SPUTNIK_EXP == 0.
 //   1: skip the MFMAs (keep LDS reads)   2: skip the operand DMA
 //   4: no LPT row order                  8: no XCD-aware tile map
-//  16: per-workgroup s_memtime phase stamps into GemmParams::debug
 //  64: every DMA re-reads the first step's tiles (cache-resident: isolates
 //      the memory system from the LDS-write / issue cost of the DMA)
 #ifndef SPUTNIK_EXP
@@ -131,9 +130,12 @@ struct GemmParams {
   // over as an fp32 partial. pair == 0: one tile per workgroup, LPT order.
   int pair;
   float *pair_partials;        // (#pairs) x (128 x BN) fp32
-  unsigned *pair_flags;        // #pairs; 1 = partial published, reset to 0
-                               // by the consumer (graph-replay safe)
-  unsigned long long *debug;   // SPUTNIK_EXP & 16 builds only: phase stamps
+  unsigned *pair_flags;        // #pairs; holds the epoch of the launch whose
+                               // producer published last (never reset)
+  unsigned pair_epoch;         // this launch's epoch (never 0)
+  unsigned *pair_error;        // set to 1 when a consumer timed out
+  int pair_fault;              // test knob: producers never publish
+  unsigned long long *debug;   // SPUTNIK_EXP & 128 builds only
   // DSS (dense = sparse x sparse): op(B)'s column lists (k-block, storage
   // block) — B's transposed metadata, or its own when op(B) = B^T.
   const int *d_offsets;
@@ -248,20 +250,6 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
   return out;
 }
 
-// Experiment builds: record (wave 0, lane 0) a per-workgroup timeline.
-// Layout per workgroup (16 slots): [realtime start, memtime start, memtime
-// prologue end, realtime loop end, memtime end (stores drained), xcc_id,
-// hw_id, k-steps, memtime after the pipeline fill, memtime after the pair
-// publish, memtime after the pipeline, memtime after the pair collect, role
-// (0 light, 1 middle, 2 heavy, 3 unpaired), memtime before the tile stores,
-// realtime end].
-__device__ __forceinline__ void exp_stamp(unsigned long long *dbg, int slot,
-                                          unsigned long long v) {
-  if constexpr ((SPUTNIK_EXP & 16) != 0) {
-    if (dbg != nullptr && threadIdx.x == 0) dbg[blockIdx.x * 16 + slot] = v;
-  }
-}
-
 // Maps the launch index to a tile index so that each XCD (blocks b and b+8
 // share one) walks a contiguous run of tiles. Bijective for any grid size.
 __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
@@ -359,7 +347,10 @@ using CfgDss = SPUTNIK_DSS_CFG;        // DSS tile configuration
 // Bounded spin for the pair hand-off (about 0.1 s): a launch can never hang
 // on a missing partial. The producer never waits and always has a lower
 // workgroup index than its consumer (in-order dispatch), so the bound is a
-// guard, not part of the protocol.
+// guard, not part of the protocol. A consumer that gives up does not use the
+// partial: it poisons its tile with NaN and raises GemmParams::pair_error
+// (read by sputnik_pair_errors()), and the per-launch epoch keeps a late
+// publish from satisfying any later launch.
 constexpr int kSpinLimit = 1 << 22;
 
 // kSparseOut: sparse output block. With kSparseIn = false that is SDD (dense
@@ -453,15 +444,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   const int row_w = kTM * wm;  // first row / col of this wave's sub-tile
   const int col_w = kTN * wn;
 
-  if constexpr ((SPUTNIK_EXP & 16) != 0) {
-    unsigned xcc, hwid;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    exp_stamp(p.debug, 0, __builtin_amdgcn_s_memrealtime());
-    exp_stamp(p.debug, 1, __builtin_amdgcn_s_memtime());
-    exp_stamp(p.debug, 5, xcc);
-    exp_stamp(p.debug, 6, hwid);
-  }
 
   // ---- per-lane DMA offsets (relative to each step's tile base) ----------
   uint32_t s_off[kSInstr], d_off[kDInstr];
@@ -789,37 +771,51 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
               (a * kFN + b) * 1024, kSc1);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (wave == kNW - 1 && lane == 0)
-        __hip_atomic_store(p.pair_flags + pair_id, 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (wave == kNW - 1 && lane == 0 && !p.pair_fault)
+        __hip_atomic_store(p.pair_flags + pair_id, p.pair_epoch,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       zero_acc();
     }
   };
-  // Consumer side: poll, barrier, add the partial (sc1 loads); the flag is
-  // reset for the next launch (stream order makes the reset visible to it).
+  // Consumer side: poll for this launch's epoch, barrier, add the partial
+  // (sc1 loads). The flag is never reset: a publish from an earlier launch
+  // carries an older epoch, so it can never satisfy this one. On timeout the
+  // partial is not used: the tile becomes NaN and the error word is raised.
   auto collect = [&]() {
     if constexpr (kPairs) {
+      int *ok = scratch + 3;
       if (tid == 0) {
         int spins = 0;
-        while (__hip_atomic_load(p.pair_flags + pair_id, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT) != 1u &&
+        bool got;
+        while (!(got = __hip_atomic_load(p.pair_flags + pair_id,
+                                         __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) ==
+                       p.pair_epoch) &&
                spins < kSpinLimit) {
           __builtin_amdgcn_s_sleep(1);
           ++spins;
         }
-        __hip_atomic_store(p.pair_flags + pair_id, 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (!got)
+          __hip_atomic_store(p.pair_error, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        *ok = got ? 1 : 0;
       }
       __syncthreads();
+      const bool got = __builtin_amdgcn_readfirstlane(*ok) != 0;
       const __amdgpu_buffer_rsrc_t rp = pair_rsrc();
       const int lb = pair_lane_base();
+      const float nan = __builtin_nanf("");
 #pragma unroll
       for (int a = 0; a < kFM; ++a)
 #pragma unroll
-        for (int b = 0; b < kFN; ++b)
-          acc[a][b] += __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                         rp, lb, (a * kFN + b) * 1024, kSc1));
+        for (int b = 0; b < kFN; ++b) {
+          if (got)
+            acc[a][b] += __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                           rp, lb, (a * kFN + b) * 1024, kSc1));
+          else
+            acc[a][b] = f32x4{nan, nan, nan, nan};
+        }
     }
   };
 
@@ -863,7 +859,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     Frags f0, f1;
     read_step(0, f0);
     wait_step(f0);
-    exp_stamp(p.debug, 8, __builtin_amdgcn_s_memtime());
     // Staggered configs: the lagging half (waves kNW/2..) passes one barrier
     // behind the leading half, and every step has two barriers, B1 before
     // the DMA/read phase and B2 before the MFMA phase, so a lagging wave's
@@ -949,7 +944,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       if constexpr (kPairs) {
         if (i + 1 == flush_at) {
           publish();
-          exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
         }
       }
       slot = nslot;
@@ -1017,7 +1011,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     Frags f0, f1;
     read_step(0, f0);
     wait_step(f0);
-    exp_stamp(p.debug, 8, __builtin_amdgcn_s_memtime());
     const bool lag = wave >= kNW / 2;
     if constexpr (SPUTNIK_LAG_PRIO != 0) {
       if (lag) __builtin_amdgcn_s_setprio(1);
@@ -1081,7 +1074,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         if constexpr (kPairs) {
           if (b + 1 == flush_blk) {
             publish();
-            exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
           }
         }
       }
@@ -1092,7 +1084,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       if constexpr (kPairs) {
         if (b + 1 == flush_blk) {
           publish();
-          exp_stamp(p.debug, 9, __builtin_amdgcn_s_memtime());
         }
       }
     };
@@ -1221,7 +1212,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         }
       }
       __syncthreads();
-      if (pass == 0) exp_stamp(p.debug, 13, __builtin_amdgcn_s_memtime());
       constexpr int kChunksPerRow = kOutCols / 8;
       constexpr int kChunks = kOutRows * kChunksPerRow;
       for (int id = tid; id < kChunks; id += kThreads) {
@@ -1307,7 +1297,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     for (int r = tid; r <= R; r += kThreads) offs[r] = p.s_offsets[r];
     if (tid == 0) scratch[2] = 0;
     __syncthreads();
-    exp_stamp(p.debug, 15, __builtin_amdgcn_s_memtime());
     for (int r = tid; r < R; r += kThreads) {
       const int nr = offs[r + 1] - offs[r];
       int rank = 0;
@@ -1409,7 +1398,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     if (hb < kMinHandoff) hb = 0;
     pair_id = panel * half + pi;
     j0 = panel * kBN;
-    exp_stamp(p.debug, 12, role);
     if (role == 0) {
       srow = rows.y;
       idx_base = e_h;
@@ -1427,7 +1415,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     }
   } else {
     // ==== one output tile per workgroup ===================================
-    exp_stamp(p.debug, 12, 3);
     const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                        : xcd_tile(blockIdx.x, gridDim.x);
     if constexpr (kGroupedSdd) {
@@ -1605,10 +1592,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   }
   setup_d(j0);
   zero_acc();
-  exp_stamp(p.debug, 2, __builtin_amdgcn_s_memtime());
   if constexpr (kDenseS) {
     const int nsteps = (p.k_limit + kBK - 1) / kBK;
-    exp_stamp(p.debug, 7, nsteps);
     // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
     // zeros through the k mask (at most 3, none when K % 128 == 0).
     if constexpr (SPUTNIK_SDD_BLOCK_LOOP != 0 && Cfg::kStagger &&
@@ -1617,7 +1602,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     else
       pipeline(0, nsteps);
   } else if constexpr (kScalarIdx) {
-    exp_stamp(p.debug, 7, p_steps);
     cached_e = -1;
     // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
     // needs 12 more address registers than it has and spills; those two
@@ -1628,18 +1612,13 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
                       p_flush > 0 ? p_flush / kStepsPerBlock : -1);
     else
       pipeline(p_first, p_steps, p_flush);
-    exp_stamp(p.debug, 10, __builtin_amdgcn_s_memtime());
     if (do_collect) collect();
-    exp_stamp(p.debug, 11, __builtin_amdgcn_s_memtime());
   } else if constexpr (kSparseD) {
-    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
     cached_e = -1;
     pipeline(0, entries * kStepsPerBlock);  // list staged by the setup
   } else {
-    exp_stamp(p.debug, 7, entries * kStepsPerBlock);
     run_sparse(entry0, 0, entries * kStepsPerBlock);
   }
-  exp_stamp(p.debug, 3, __builtin_amdgcn_s_memrealtime());
   bool empty = false;
   if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
   if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
@@ -1647,12 +1626,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     write_zero_tile();
   else
     write_tile(out_block);
-  if constexpr ((SPUTNIK_EXP & 16) != 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  exp_stamp(p.debug, 4, __builtin_amdgcn_s_memtime());
-  exp_stamp(p.debug, 14, __builtin_amdgcn_s_memrealtime());
   if constexpr ((SPUTNIK_EXP & 128) != 0) {
     if (p.debug != nullptr && lane == 0 && (wave == 0 || wave == kNW / 2)) {
       unsigned long long *o =

@@ -205,6 +205,27 @@ int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream) {
   return sputnik::block::Transpose(ToCpp(a), static_cast<hipStream_t>(stream));
 }
 
+int sputnik_bitmask(const sputnik_block_matrix_t *m, void *stream) {
+  if (!m || !m->bitmask) return hipErrorInvalidValue;
+  const bool trans = m->offsets_t != nullptr;
+  if ((trans ? !m->indices_t : !m->offsets) ||
+      (m->nonzeros > 0 && !(trans ? m->indices_t : m->indices)))
+    return hipErrorInvalidValue;
+  if (m->block_size != 128 && m->block_size != 64 && m->block_size != 32 &&
+      m->block_size != 16)
+    return hipErrorNotSupported;
+  return sputnik::block::Bitmask(ToCpp(m), static_cast<hipStream_t>(stream));
+}
+
+size_t sputnik_bitmask_bytes(const sputnik_block_matrix_t *m) {
+  if (!m) return 0;
+  const int b = m->block_size;
+  if (b != 128 && b != 64 && b != 32 && b != 16) return 0;
+  const bool trans = m->offsets_t != nullptr;
+  return sputnik::block::BitMatrix::SizeInBytes(
+      (trans ? m->cols : m->rows) / b, (trans ? m->rows : m->cols) / b);
+}
+
 int sputnik_mask_to_bcsr(const uint8_t *mask, int block_rows, int block_cols,
                          int32_t *offsets, int16_t *indices, void *stream) {
   if (!offsets || (block_rows > 0 && block_cols > 0 && (!mask || !indices)))
@@ -232,6 +253,20 @@ int sputnik_can_implement(int op, const void *a, int transpose_a,
              : 0;
 }
 
+int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
+                     const sputnik_matrix_t *b, int transpose_b,
+                     const sputnik_block_matrix_t *c) {
+  if (!a || !b || !c) return -1;
+  const Matrix ca = ToCpp(a), cb = ToCpp(b);
+  const BlockMatrix cc = ToCpp(c);
+  return sputnik_amd::SddPlan(&ca, transpose_a != 0, &cb, transpose_b != 0,
+                              &cc);
+}
+
+int sputnik_pair_errors(void) { return sputnik_amd::PairErrors(); }
+
+void sputnik_debug_pair_fault(int on) { sputnik_amd::SetPairFault(on); }
+
 size_t sputnik_abi_block_matrix_size(void) { return sizeof(BlockMatrix); }
 
 size_t sputnik_abi_block_matrix_offset(int field) {
@@ -255,6 +290,10 @@ size_t sputnik_abi_block_matrix_offset(int field) {
 
 size_t sputnik_abi_matrix_size(void) { return sizeof(Matrix); }
 
-const char *sputnik_version(void) { return "sputnik-amd 0.1 (gfx950)"; }
+#ifndef SPUTNIK_BUILD_HASH
+#define SPUTNIK_BUILD_HASH "unknown"
+#endif
+const char *sputnik_version(void) { return "sputnik-amd 0.2 (gfx950)"; }
+const char *sputnik_build_hash(void) { return SPUTNIK_BUILD_HASH; }
 
 }  // extern "C"

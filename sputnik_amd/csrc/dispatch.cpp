@@ -29,27 +29,48 @@
 
 namespace sputnik_amd {
 
-// Experiment builds (SPUTNIK_EXP & 16) copy this into GemmParams::debug.
+// Experiment builds (SPUTNIK_EXP & 128) copy this into GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
 
+// Compute units of a device, queried once per device (every SDD and every
+// pair-eligible DSD/DDS call needs it).
+static int DeviceCUs(int dev) {
+  constexpr int kMaxDevices = 64;
+  static int cached[kMaxDevices] = {};
+  if (dev < 0 || dev >= kMaxDevices) return 0;
+  int cus = __atomic_load_n(&cached[dev], __ATOMIC_RELAXED);
+  if (cus > 0) return cus;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
+                            dev) != hipSuccess || cus <= 0)
+    return 0;
+  __atomic_store_n(&cached[dev], cus, __ATOMIC_RELAXED);
+  return cus;
+}
+
 // ---- pair-balancing workspace ---------------------------------------------
-// fp32 partial slots + hand-off flags, one set per (device, stream) so
-// concurrent streams never share them. Allocated on the first eligible call
-// and kept for the life of the process (like a BLAS handle's workspace);
-// never allocated while the stream is being captured into a graph (that call
-// runs one tile per workgroup instead). Flags return to 0 inside every
-// launch, so captured launches replay correctly.
+// fp32 partial slots + hand-off flags + an error word, one set per (device,
+// stream) so concurrent streams never share them. Allocated on the first
+// eligible call and kept for the life of the process (like a BLAS handle's
+// workspace). One workspace per stream relies on stream order: launches on
+// one stream never overlap, so each launch owns the slots while it runs.
+// Every launch carries a new epoch; a consumer waits for its own epoch, so a
+// flag left by an earlier launch (or by a producer that published after its
+// consumer gave up) can never satisfy a later launch, and nothing has to be
+// reset. A launch captured into a graph would replay one baked-in epoch
+// (and could replay on another stream), so pairs are off while capturing.
 struct PairSlot {
   int device = -1;
   hipStream_t stream = nullptr;
   float *partials = nullptr;
-  unsigned *flags = nullptr;
+  unsigned *flags = nullptr;  // [pairs] flags, then the error word
+  unsigned epoch = 0;
   int pairs = 0;  // capacity
   int slots = 0;  // resident workgroups on the device
 };
 constexpr int kMaxPairSlots = 16;
 static PairSlot g_pairs[kMaxPairSlots];
 static std::mutex g_pairs_mu;
+static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
 
 static bool PairsEnabled() {
 #ifdef SPUTNIK_NO_PAIRS
@@ -76,6 +97,10 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   if (!CfgSparse::kStagger || CfgSparse::kWGs != 1) return;
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+      cs != hipStreamCaptureStatusNone)
+    return;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
@@ -86,20 +111,14 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
       break;
     }
   if (slot == nullptr) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
-        cs != hipStreamCaptureStatusNone)
-      return;
     for (auto &s : g_pairs)
       if (s.partials == nullptr) {
         slot = &s;
         break;
       }
     if (slot == nullptr) return;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
-                              dev) != hipSuccess || cus <= 0)
-      return;
+    const int cus = DeviceCUs(dev);
+    if (cus <= 0) return;
     const int slots = cus * CfgSparse::kWGs;
     const int pairs = slots / 2;
     float *partials = nullptr;
@@ -107,8 +126,9 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     if (hipMalloc(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
                                  sizeof(float)) != hipSuccess)
       return;
-    if (hipMalloc(&flags, pairs * sizeof(unsigned)) != hipSuccess ||
-        hipMemset(flags, 0, pairs * sizeof(unsigned)) != hipSuccess) {
+    const size_t flag_bytes = (pairs + 1) * sizeof(unsigned);
+    if (hipMalloc(&flags, flag_bytes) != hipSuccess ||
+        hipMemset(flags, 0, flag_bytes) != hipSuccess) {
       (void)hipFree(partials);
       if (flags) (void)hipFree(flags);
       return;
@@ -121,10 +141,42 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     slot->slots = slots;
   }
   if (p->num_tiles > slot->slots) return;
+  if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
   p->pair = 1;
   p->pair_partials = slot->partials;
   p->pair_flags = slot->flags;
+  p->pair_epoch = slot->epoch;
+  p->pair_error = slot->flags + slot->pairs;
+  p->pair_fault = g_pair_fault;
 }
+
+// Pair hand-offs that timed out since the last call, over every workspace of
+// the current device (synchronizes each workspace's stream); the error words
+// are cleared.
+int PairErrors() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  int total = 0;
+  for (auto &s : g_pairs) {
+    if (s.partials == nullptr || s.device != dev) continue;
+    unsigned word = 0;
+    if (hipStreamSynchronize(s.stream) != hipSuccess ||
+        hipMemcpy(&word, s.flags + s.pairs, sizeof(word),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return -1;
+    if (word != 0) {
+      ++total;
+      const unsigned zero = 0;
+      if (hipMemcpy(s.flags + s.pairs, &zero, sizeof(zero),
+                    hipMemcpyHostToDevice) != hipSuccess)
+        return -1;
+    }
+  }
+  return total;
+}
+
+void SetPairFault(int on) { g_pair_fault = on != 0; }
 
 namespace {
 
@@ -430,11 +482,10 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   if (disabled || c.offsets == nullptr) return false;
   constexpr int kGrp = CfgSddGrouped::kBN / kBlock;
   const int blocks = p->num_tiles;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount,
-                            dev) != hipSuccess)
-    return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const int cus = DeviceCUs(dev);
+  if (cus <= 0) return false;
   // Below ~6 blocks per CU the k-split block tile is faster (SDD 8192^2 x
   // 8192, scripts/exp_grp.sh: 4 per CU 320 vs 367 us grouped; 8 per CU
   // 656 vs 577 us).
@@ -756,6 +807,21 @@ hipError_t RowIndices(BlockMatrix a, short *row_indices, hipStream_t stream) {
                                        row_indices, stream);
 }
 
+hipError_t Bitmask(BlockMatrix m, hipStream_t stream) {
+  // bitmask.cu:8-16: the orientation follows offsets_t.
+  const bool trans = m.offsets_t != nullptr;
+  const int b = AsInt(m.block_size);
+  if (b == 0) return hipErrorNotSupported;
+  SPUTNIK_CHECK(m.bitmask);
+  const int block_rows = (trans ? m.cols : m.rows) / b;
+  const int block_cols = (trans ? m.rows : m.cols) / b;
+  return sputnik_amd::LaunchBitmask(
+      block_rows, block_cols,
+      static_cast<const int *>(trans ? m.offsets_t : m.offsets),
+      static_cast<const short *>(trans ? m.indices_t : m.indices),
+      static_cast<unsigned long long *>(m.bitmask), stream);
+}
+
 hipError_t Transpose(BlockMatrix a, hipStream_t stream) {
   // transpose.cu:107-109 checks the three workspaces; with no nonzero block
   // the two per-block ones are legitimately empty.
@@ -773,6 +839,16 @@ hipError_t Transpose(BlockMatrix a, hipStream_t stream) {
 namespace sputnik_amd {
 
 int StatusCode(Status st) { return AsCode(st); }
+
+int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
+  if (!a || !b || !c) return -1;
+  GemmParams p;
+  const BlockMatrix &cm = *static_cast<const BlockMatrix *>(c);
+  if (PrepareSdd(*static_cast<const Matrix *>(a), ta,
+                 *static_cast<const Matrix *>(b), tb, cm, &p) != Status::kOk)
+    return -1;
+  return UseGroupedSdd(&p, cm, tb) ? 1 : 0;
+}
 
 // Host-only acceptance test (no launch, no device needed): op 0 = DSD
 // (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block), 3 = SSD
@@ -815,8 +891,8 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 
 }  // namespace sputnik_amd
 
-// Experiment hook (not part of include/sputnik_amd.h): phase-stamp buffer
-// for SPUTNIK_EXP & 16 builds; 8 x u64 per workgroup.
+// Experiment hook (not part of include/sputnik_amd.h): per-segment cycle
+// sums of SPUTNIK_EXP & 128 builds.
 extern "C" void sputnik_exp_set_debug(void *buffer) {
   sputnik_amd::g_debug = static_cast<unsigned long long *>(buffer);
 }

@@ -11,6 +11,12 @@ hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
                                    int *offsets_t, short *indices_t,
                                    int *block_offsets, hipStream_t stream);
 
+// BitMatrix of a BCSR topology (reference bitmask.cu:7-45): block_rows x
+// ceil(block_cols / 64) uint64 words, zeroed and then filled.
+hipError_t LaunchBitmask(int block_rows, int block_cols, const int *offsets,
+                         const short *indices, unsigned long long *bitmask,
+                         hipStream_t stream);
+
 hipError_t LaunchRowIndices(int block_rows, const int *offsets,
                             short *row_indices, hipStream_t stream);
 

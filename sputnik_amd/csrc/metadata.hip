@@ -9,10 +9,12 @@
 // Stability: blocks of one column keep storage order. Storage order is
 // block-row order, and a valid BCSR row holds each column at most once, so the
 // rank of a block inside its column equals the number of earlier block-rows
-// that hold that column. The kernel walks block-rows in order and hands out
-// positions from per-column cursors in LDS, one block-row per step; within a
-// step every block touches a different cursor, so no atomics are needed.
-//
+// that hold that column. Each workgroup owns a slice of block-columns and
+// builds, in LDS, the slice's column-major bit matrix (bit r of column c set
+// when block-row r holds c) plus a per-word prefix count; a block's rank is
+// then one prefix lookup plus one popcount, with no ordering between threads
+// and no communication between workgroups (each counts the blocks left of
+// its slice itself).
 // RowIndices: replaces reference sputnik/block/row_indices/row_indices.cu:7-36
 // (row_indices[k] = m for k in [offsets[m], offsets[m+1])).
 //
@@ -26,34 +28,94 @@ namespace sputnik_amd {
 namespace {
 
 constexpr int kTransposeThreads = 1024;
+constexpr int kTransposeWaves = kTransposeThreads / 64;
 constexpr int kMaxBlockCols = 32768;  // int16 block-column indices
+// LDS words (32 rows each) of one slice: bit words + their prefix counts.
+constexpr int kTransposeWords = 16384;
+
+// Calls f(row, entry, column) for every stored block of `slice` columns
+// [c0, c1), one wave per block-row.
+template <typename F>
+__device__ __forceinline__ void for_slice_blocks(int block_rows,
+                                                 const int *offsets,
+                                                 const short *indices, int c0,
+                                                 int c1, F f) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  for (int r = wave; r < block_rows; r += kTransposeWaves) {
+    const int k1 = offsets[r + 1];
+    for (int k = offsets[r] + lane; k < k1; k += 64) {
+      const int c = indices[k];
+      if (c >= c0 && c < c1) f(r, k, c);
+    }
+  }
+}
 
 __global__ void __launch_bounds__(kTransposeThreads)
-    transpose_metadata_kernel(int block_rows, int block_cols,
+    transpose_metadata_kernel(int block_rows, int block_cols, int slice,
                               const int *__restrict__ offsets,
                               const short *__restrict__ indices,
                               int *__restrict__ offsets_t,
                               short *__restrict__ indices_t,
                               int *__restrict__ block_offsets) {
-  __shared__ int cursor[kMaxBlockCols];
+  __shared__ unsigned bits[kTransposeWords];
+  __shared__ int prefix[kTransposeWords];
   __shared__ int partial[kTransposeThreads];
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int words = (block_rows + 31) >> 5;  // per column
+  const int c0 = blockIdx.x * slice;
+  const int c1 = min(c0 + slice, block_cols);
+  const int ncols = c1 - c0;
   const int blocks = offsets[block_rows];
 
-  // 1. Histogram of block-columns.
-  for (int c = tid; c < block_cols; c += kTransposeThreads) cursor[c] = 0;
-  __syncthreads();
+  // 1. Bit matrix of the slice; blocks left of the slice (the slice's base).
+  for (int w = tid; w < ncols * words; w += kTransposeThreads) bits[w] = 0;
+  int left = 0;
   for (int k = tid; k < blocks; k += kTransposeThreads)
-    atomicAdd(&cursor[indices[k]], 1);
+    left += indices[k] < c0 ? 1 : 0;
+  partial[tid] = left;
+  __syncthreads();
+  for_slice_blocks(block_rows, offsets, indices, c0, c1,
+                   [&](int r, int, int c) {
+                     atomicOr(&bits[(c - c0) * words + (r >> 5)],
+                              1u << (r & 31));
+                   });
+  // Block sum of `left` (tree over partial[]).
+  for (int stride = kTransposeThreads / 2; stride > 0; stride >>= 1) {
+    __syncthreads();
+    if (tid < stride) partial[tid] += partial[tid + stride];
+  }
+  __syncthreads();
+  const int base = partial[0];
   __syncthreads();
 
-  // 2. Exclusive scan -> offsets_t; cursor[c] = first slot of column c.
-  const int per = (block_cols + kTransposeThreads - 1) / kTransposeThreads;
-  const int c0 = min(tid * per, block_cols);
-  const int c1 = min(c0 + per, block_cols);
-  int sum = 0;
-  for (int c = c0; c < c1; ++c) sum += cursor[c];
-  partial[tid] = sum;
+  // 2. Per-column word prefix counts (one wave per column, 64 words a pass)
+  //    and column totals.
+  const int wave = tid >> 6;
+  for (int cl = wave; cl < ncols; cl += kTransposeWaves) {
+    int run = 0;
+    for (int w0 = 0; w0 < words; w0 += 64) {
+      const int w = w0 + lane;
+      const int n = w < words ? __popc(bits[cl * words + w]) : 0;
+      int incl = n;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += v;
+      }
+      if (w < words) prefix[cl * words + w] = run + incl - n;
+      run += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) partial[cl] = run;  // ncols <= kTransposeThreads
+  }
+  __syncthreads();
+
+  // 3. Exclusive scan of the column totals -> offsets_t (slice <= threads:
+  //    thread t owns column c0 + t).
+  const int mine = tid < ncols ? partial[tid] : 0;
+  __syncthreads();
+  partial[tid] = mine;
   __syncthreads();
   for (int stride = 1; stride < kTransposeThreads; stride <<= 1) {
     const int v = tid >= stride ? partial[tid - stride] : 0;
@@ -61,28 +123,46 @@ __global__ void __launch_bounds__(kTransposeThreads)
     partial[tid] += v;
     __syncthreads();
   }
-  int run = partial[tid] - sum;  // exclusive prefix of this thread's range
-  for (int c = c0; c < c1; ++c) {
-    const int n = cursor[c];
-    cursor[c] = run;
-    offsets_t[c] = run;
-    run += n;
+  const int first = base + partial[tid] - mine;
+  __syncthreads();
+  if (tid < ncols) {
+    partial[tid] = first;  // first slot of column c0 + tid
+    offsets_t[c0 + tid] = first;
   }
-  if (tid == 0) offsets_t[block_cols] = blocks;
+  if (c1 == block_cols && tid == 0) offsets_t[block_cols] = blocks;
   __syncthreads();
 
-  // 3. Stable scatter, one block-row at a time.
-  for (int r = 0; r < block_rows; ++r) {
-    const int k0 = offsets[r];
-    const int k1 = offsets[r + 1];
-    for (int k = k0 + tid; k < k1; k += kTransposeThreads) {
-      const int c = indices[k];
-      const int pos = cursor[c];
-      cursor[c] = pos + 1;
-      indices_t[pos] = static_cast<short>(r);
-      block_offsets[pos] = k;
-    }
-    __syncthreads();
+  // 4. Scatter: slot = column start + rank of the block-row in its column.
+  for_slice_blocks(block_rows, offsets, indices, c0, c1,
+                   [&](int r, int k, int c) {
+                     const int cl = c - c0;
+                     const int w = cl * words + (r >> 5);
+                     const int rank =
+                         prefix[w] + __popc(bits[w] & ((1u << (r & 31)) - 1u));
+                     const int pos = partial[cl] + rank;
+                     indices_t[pos] = static_cast<short>(r);
+                     block_offsets[pos] = k;
+                   });
+}
+
+// ---- Bitmask (reference sputnik/block/bitmask/bitmask.cu:7-45 with the
+// BitMatrix layout of bit_matrix.h:14-40): a row-major bit matrix of
+// ceil(cols/64) uint64 words per block-row, bit j % 64 of word j / 64 set
+// when the row holds block-column j. The words are zeroed by the launcher;
+// one wave per block-row ORs its blocks in.
+__global__ void __launch_bounds__(256)
+    bitmask_kernel(int block_rows, int words_per_row,
+                   const int *__restrict__ offsets,
+                   const short *__restrict__ indices,
+                   unsigned long long *__restrict__ bitmask) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= block_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int k1 = offsets[r + 1];
+  for (int k = offsets[r] + lane; k < k1; k += 64) {
+    const int j = indices[k];
+    atomicOr(bitmask + (long long)r * words_per_row + (j >> 6),
+             1ull << (j & 63));
   }
 }
 
@@ -230,10 +310,35 @@ hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
                                    int *block_offsets, hipStream_t stream) {
   if (block_cols > kMaxBlockCols || block_rows < 0 || block_cols < 0)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(transpose_metadata_kernel, dim3(1),
+  if (block_cols == 0)
+    return hipMemsetAsync(offsets_t, 0, sizeof(int), stream);
+  const int words = (block_rows + 31) / 32;
+  // Columns per workgroup: the slice's bit words and prefixes fit in LDS,
+  // and its column totals fit one per thread.
+  int slice = words == 0 ? block_cols : kTransposeWords / words;
+  slice = slice < 1 ? 1 : slice;
+  slice = slice > kTransposeThreads ? kTransposeThreads : slice;
+  slice = slice > block_cols ? block_cols : slice;
+  const int grid = (block_cols + slice - 1) / slice;
+  hipLaunchKernelGGL(transpose_metadata_kernel, dim3(grid),
                      dim3(kTransposeThreads), 0, stream, block_rows,
-                     block_cols, offsets, indices, offsets_t, indices_t,
+                     block_cols, slice, offsets, indices, offsets_t, indices_t,
                      block_offsets);
+  return hipGetLastError();
+}
+
+hipError_t LaunchBitmask(int block_rows, int block_cols, const int *offsets,
+                         const short *indices, unsigned long long *bitmask,
+                         hipStream_t stream) {
+  if (block_rows < 0 || block_cols < 0 || block_cols > kMaxBlockCols)
+    return hipErrorInvalidValue;
+  const int words = (block_cols + 63) / 64;
+  const size_t bytes = (size_t)words * block_rows * sizeof(unsigned long long);
+  if (bytes == 0) return hipSuccess;
+  const hipError_t e = hipMemsetAsync(bitmask, 0, bytes, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(bitmask_kernel, dim3((block_rows + 3) / 4), dim3(256), 0,
+                     stream, block_rows, words, offsets, indices, bitmask);
   return hipGetLastError();
 }
 

@@ -41,6 +41,8 @@ def test_cpp_api_symbols_exported():
         "_ZN7sputnik5block6MatmulENS0_6MatrixEbS1_bNS0_11BlockMatrixEP12ihipStream_t",
         "_ZN7sputnik5block10RowIndicesENS0_11BlockMatrixEPsP12ihipStream_t",
         "_ZN7sputnik5block9TransposeENS0_11BlockMatrixEP12ihipStream_t",
+        # bitmask.h:10
+        "_ZN7sputnik5block7BitmaskENS0_11BlockMatrixEP12ihipStream_t",
         # SSD (ssd.h:10-22) and SDS (sds.h:10-22)
         "_ZN7sputnik5block6MatmulENS0_11BlockMatrixEbNS0_6MatrixEbS1_P12ihipStream_t",
         "_ZN7sputnik5block8MatmulExENS0_11BlockMatrixEbNS0_6MatrixEbS1_P12ihipStream_t",
@@ -126,3 +128,19 @@ def test_can_implement_dds_sdd(ta, tb):
 
 def test_version():
     assert "gfx950" in sp.version()
+
+
+def test_build_hash_matches_sources():
+    """The library in the tree was built from the sources in the tree."""
+    from sputnik_amd import srchash
+    assert sp.build_hash() == srchash.source_hash()
+
+
+@pytest.mark.parametrize("trans", [False, True])
+def test_bitmask_bytes(trans):
+    """reference bitmask.h:16-23 / bit_matrix.h:14-17: rows of ceil(cols/64)
+    uint64 words, over the transposed orientation when offsets_t is set."""
+    a = bm(3 * 128, 70 * 128, 5, **({"offsets_t": _T()} if trans else {}))
+    rows, cols = (70, 3) if trans else (3, 70)
+    words = (cols + 63) // 64
+    assert sp.lib().sputnik_bitmask_bytes(ctypes.byref(a._c())) == rows * words * 8

@@ -1,0 +1,340 @@
+"""Exact-arithmetic known-answer tests: every product, every transpose, both
+element types, compared BIT-EXACTLY with a closed-form result.
+
+The reference ships no golden vectors, so these KATs pin the
+kernels independently of the CPU oracle: all operand values are small
+integers (-1, 0, 1), so every product and every partial sum of the fp32
+accumulation is an exact integer whatever the summation order (|sum| <= K <
+2^24), and the final fp16 / bf16 rounding is exact too (|sum| <= K <= 2048
+for fp16, K <= 256 for bf16). The expected output is the float64 product of
+the same integer matrices (numpy on the host), converted exactly; the test
+is torch.equal on the whole output (value equality: +0 and -0 compare
+equal). The shapes reach every dispatch path: pair balancing (4096^2 with
+one tile per CU), tall operands, partial N/M/K tiles, the grouped SDD
+(>= 6 blocks per CU, checked with sputnik_sdd_plan), transposed metadata
+built by Matmul (device Transpose) and precomputed for MatmulEx.
+Reference test structure: sputnik/block/dsd/dsd_test.cu:68-194,
+sdd_test.cu:71-89 (same products, tolerance replaced by equality).
+"""
+
+import numpy as np
+import pytest
+
+from sputnik_amd import matrix_utils as mu
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # collected here, skipped: no device
+    pytest.skip("no GPU", allow_module_level=True)
+
+import sputnik_amd as sp  # noqa: E402
+
+sp.lib()  # fail loudly if the native library is missing
+
+B = mu.BLOCK
+TD = {"f16": torch.float16, "bf16": torch.bfloat16}
+TRANSPOSES = [(False, False), (False, True), (True, False), (True, True)]
+
+
+def _ints(rng, shape):
+    return rng.integers(-1, 2, size=shape).astype(np.float32)
+
+
+class ISparse:
+    """BCSR operand with integer values: host dense copy + device matrix."""
+
+    def __init__(self, rows, cols, density, rng, dtype, unordered=True,
+                 nb=None, topology=None):
+        self.rows, self.cols = rows, cols
+        if topology is not None:
+            self.offsets, self.indices = topology
+            nb = int(self.offsets[-1])
+        else:
+            if nb is None:
+                nb = mu.nonzeros_for_density(rows, cols, density) // (B * B)
+            self.offsets, self.indices = mu.random_topology(
+                rows // B, cols // B, nb, rng, unordered=unordered)
+        self.values = _ints(rng, (nb, B, B))
+        self.dense = mu.to_dense(rows, cols, self.offsets, self.indices,
+                                 self.values)
+        self.dev = torch.from_numpy(self.values).to(TD[dtype]).cuda()
+        self.m = sp.BlockMatrix(
+            rows, cols, 128, nb * B * B, self.dev,
+            torch.from_numpy(self.offsets.astype(np.int32)).cuda(),
+            torch.from_numpy(self.indices.astype(np.int16)).cuda())
+        sp.AllocateTransposeBuffers(self.m)
+
+    def blocks_of(self, full):
+        """The stored blocks of `full` (dense [rows, cols]) at this topology."""
+        rows = np.repeat(np.arange(len(self.offsets) - 1), np.diff(self.offsets))
+        return np.stack([full[r * B:(r + 1) * B, c * B:(c + 1) * B]
+                         for r, c in zip(rows, self.indices)]) \
+            if len(rows) else np.zeros((0, B, B))
+
+
+class IDense:
+    def __init__(self, rows, cols, rng, dtype):
+        self.values = _ints(rng, (rows, cols))
+        self.dev = torch.from_numpy(self.values).to(TD[dtype]).cuda()
+        self.m = sp.Matrix(rows, cols, self.dev)
+
+
+def _op(x, t):
+    return x.T if t else x
+
+
+def _expect(x64, dtype):
+    return torch.from_numpy(np.ascontiguousarray(x64)).to(TD[dtype]).cuda()
+
+
+def _equal(got, want, what):
+    torch.cuda.synchronize()
+    if not torch.equal(got, want):
+        bad = (got != want)
+        n = int(bad.sum())
+        idx = bad.nonzero()[0].tolist()
+        raise AssertionError(f"{what}: {n} of {got.numel()} elements differ, "
+                             f"first at {idx}: got {got[tuple(idx)].item()} "
+                             f"want {want[tuple(idx)].item()}")
+
+
+def _nan_out(rows, cols, dtype):
+    t = torch.full((rows, cols), float("nan"), dtype=TD[dtype], device="cuda")
+    return sp.Matrix(rows, cols, t), t
+
+
+# ------------------------------------------------------------------ DSD --
+
+def kat_dsd(m, k, n, density, ta, tb, dtype, ex=False, seed=0,
+            topology=None):
+    rng = np.random.default_rng(seed)
+    A = ISparse(*((k, m) if ta else (m, k)), density, rng, dtype,
+                topology=topology)
+    Bd = IDense(*((n, k) if tb else (k, n)), rng, dtype)
+    C, c_t = _nan_out(m, n, dtype)
+    if ex:
+        sp.Transpose(A.m)
+        sp.MatmulEx(A.m, ta, Bd.m, tb, C)
+    else:
+        sp.Matmul(A.m, ta, Bd.m, tb, C)
+    want = _op(A.dense, ta).astype(np.float64) @ _op(Bd.values, tb)
+    return c_t, _expect(want, dtype), (A, Bd, C)
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("dtype,k", [("f16", 1024), ("bf16", 256)])
+def test_kat_dsd(ta, tb, dtype, k):
+    got, want, _ = kat_dsd(1024, k, 1032, 0.5, ta, tb, dtype)
+    _equal(got, want, f"dsd {ta}{tb} {dtype}")
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+def test_kat_dsd_ex_tall(ta, tb):
+    """> 256 block-rows (tall tile config), MatmulEx with precomputed
+    metadata, partial N tile."""
+    got, want, _ = kat_dsd(300 * 128, 384, 264, 0.3, ta, tb, "f16", ex=True)
+    _equal(got, want, f"dsd tall {ta}{tb}")
+
+
+@pytest.mark.parametrize("ta", [False, True])
+def test_kat_dsd_4096_pairs(ta):
+    """BASELINE config 2 shape (4096^3, 50%): one tile per CU, the
+    pair-balancing hand-offs between workgroups are exercised."""
+    got, want, _ = kat_dsd(4096, 4096, 4096, 0.5, ta, False, "f16", seed=3)
+    _equal(got, want, f"dsd 4096 ta={ta}")
+    assert sp.pair_errors() == 0
+
+
+# ------------------------------------------------------------------ DDS --
+
+def kat_dds(m, k, n, density, ta, tb, dtype, ex=False, seed=0):
+    rng = np.random.default_rng(seed)
+    A = IDense(*((k, m) if ta else (m, k)), rng, dtype)
+    Bs = ISparse(*((n, k) if tb else (k, n)), density, rng, dtype)
+    C, c_t = _nan_out(m, n, dtype)
+    if ex:
+        sp.Transpose(Bs.m)
+        sp.MatmulEx(A.m, ta, Bs.m, tb, C)
+    else:
+        sp.Matmul(A.m, ta, Bs.m, tb, C)
+    want = _op(A.values, ta).astype(np.float64) @ _op(Bs.dense, tb)
+    return c_t, _expect(want, dtype)
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("dtype,k", [("f16", 1024), ("bf16", 256)])
+def test_kat_dds(ta, tb, dtype, k):
+    got, want = kat_dds(1032, k, 1024, 0.5, ta, tb, dtype)
+    _equal(got, want, f"dds {ta}{tb} {dtype}")
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+def test_kat_dds_ex_tall(ta, tb):
+    got, want = kat_dds(264, 384, 300 * 128, 0.3, ta, tb, "f16", ex=True)
+    _equal(got, want, f"dds tall {ta}{tb}")
+
+
+def test_kat_dds_4096_pairs():
+    got, want = kat_dds(4096, 4096, 4096, 0.5, False, False, "f16", seed=4)
+    _equal(got, want, "dds 4096")
+    assert sp.pair_errors() == 0
+
+
+# ------------------------------------------------------------------ SDD --
+
+def kat_sdd(m, k, n, density, ta, tb, dtype, nb=None, seed=0):
+    rng = np.random.default_rng(seed)
+    A = IDense(*((k, m) if ta else (m, k)), rng, dtype)
+    Bd = IDense(*((n, k) if tb else (k, n)), rng, dtype)
+    Cs = ISparse(m, n, density, rng, dtype, nb=nb)
+    Cs.dev.fill_(float("nan"))
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    plan = sp.sdd_plan(A.m, ta, Bd.m, tb, Cs.m)
+    sp.Matmul(A.m, ta, Bd.m, tb, Cs.m)
+    full = _op(A.values, ta).astype(np.float64) @ _op(Bd.values, tb)
+    return Cs.dev, _expect(Cs.blocks_of(full), dtype), plan
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("dtype,k", [("f16", 1032), ("bf16", 200)])
+def test_kat_sdd(ta, tb, dtype, k):
+    got, want, plan = kat_sdd(1024, k, 1024, 0.5, ta, tb, dtype)
+    assert plan == 0
+    _equal(got, want, f"sdd {ta}{tb} {dtype}")
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("k", [256, 200])
+def test_kat_sdd_grouped(ta, tb, k):
+    """6 x CUs + 37 output blocks: the grouped 128x512 SDD tiles (asserted
+    through the dispatcher's plan), with the last partial group of a row,
+    unordered columns and a K tail (k=200)."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nb = 6 * cus + 37
+    side = 128 * int(np.ceil(np.sqrt(nb / 0.6)))
+    got, want, plan = kat_sdd(side, k, side, None, ta, tb, "f16", nb=nb,
+                              seed=k + 2 * ta + tb)
+    assert plan == 1, "grouped SDD tiles not selected"
+    _equal(got, want, f"sdd grouped {ta}{tb} k={k}")
+
+
+def test_sdd_plan_threshold():
+    """Just below 6 blocks per CU the k-split block tile is chosen."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(1)
+    side = 128 * 64
+    for nb, want in ((6 * cus - 1, 0), (6 * cus, 1)):
+        A = IDense(side, 128, rng, "f16")
+        Bd = IDense(128, side, rng, "f16")
+        Cs = ISparse(side, side, None, rng, "f16", nb=nb)
+        assert sp.sdd_plan(A.m, False, Bd.m, False, Cs.m) == -1  # no row_indices
+        sp.AllocateRowIndicesBuffer(Cs.m)
+        assert sp.sdd_plan(A.m, False, Bd.m, False, Cs.m) == want, nb
+
+
+# ------------------------------------------------------------ SSD / SDS --
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("op", ["ssd", "sds"])
+def test_kat_ss(op, ta, tb):
+    rng = np.random.default_rng(ta * 2 + tb)
+    m, k, n = 1024, 768, 1152
+    dtype = "f16"
+    if op == "ssd":
+        X = ISparse(*((k, m) if ta else (m, k)), 0.5, rng, dtype)
+        Y = IDense(*((n, k) if tb else (k, n)), rng, dtype)
+        full = _op(X.dense, ta).astype(np.float64) @ _op(Y.values, tb)
+    else:
+        X = IDense(*((k, m) if ta else (m, k)), rng, dtype)
+        Y = ISparse(*((n, k) if tb else (k, n)), 0.5, rng, dtype)
+        full = _op(X.values, ta).astype(np.float64) @ _op(Y.dense, tb)
+    Cs = ISparse(m, n, 0.3, rng, dtype)
+    Cs.dev.fill_(float("nan"))
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    sp.Matmul(X.m, ta, Y.m, tb, Cs.m)
+    _equal(Cs.dev, _expect(Cs.blocks_of(full), dtype), f"{op} {ta}{tb}")
+
+
+# ------------------------------------------------------------------ DSS --
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("dtype,k", [("f16", 1024), ("bf16", 256)])
+def test_kat_dss(ta, tb, dtype, k):
+    rng = np.random.default_rng(10 + ta * 2 + tb)
+    m, n = 896, 1024
+    X = ISparse(*((k, m) if ta else (m, k)), 0.5, rng, dtype)
+    Y = ISparse(*((n, k) if tb else (k, n)), 0.5, rng, dtype)
+    C, c_t = _nan_out(m, n, dtype)
+    sp.Matmul(X.m, ta, Y.m, tb, C)
+    want = _op(X.dense, ta).astype(np.float64) @ _op(Y.dense, tb)
+    _equal(c_t, _expect(want, dtype), f"dss {ta}{tb} {dtype}")
+
+
+# ------------------------------------------- pair hand-off robustness --
+
+def _skewed_rows(rng, rows_b=32, cols_b=32):
+    """Block-rows alternating 28 and 4 blocks (mean 16): every heavy row
+    hands 12 blocks to its light partner under pair balancing."""
+    counts = np.where(np.arange(rows_b) % 2 == 0, 28, 4)
+    offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    indices = np.concatenate([np.sort(rng.choice(cols_b, c, replace=False))
+                              for c in counts]).astype(np.int16)
+    return offsets, indices
+
+
+def test_pair_timeout_fails_loudly():
+    """A pair producer that never publishes (test knob) makes its consumer
+    time out: the consumer's tile is NaN (never a stale partial), the error
+    is reported by sputnik_pair_errors(), and the next launch on the same
+    workspace is exact again (per-launch epochs, no flag to reset)."""
+    rng = np.random.default_rng(5)
+    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, None, False, False,
+                                    "f16", seed=5, topology=_skewed_rows(rng))
+    _equal(got, want, "dsd before fault")
+    assert sp.pair_errors() == 0
+    sp.lib().sputnik_debug_pair_fault(1)
+    try:
+        got.fill_(0)
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+        torch.cuda.synchronize()
+    finally:
+        sp.lib().sputnik_debug_pair_fault(0)
+    nan_rows = torch.isnan(got.float()).any(dim=1)
+    assert int(nan_rows.sum()) > 0, "no consumer tile was poisoned"
+    assert sp.pair_errors() > 0
+    assert sp.pair_errors() == 0  # cleared by the previous call
+    ok = ~nan_rows
+    assert torch.equal(got[ok], want[ok])  # tiles without a hand-off exact
+    got.fill_(float("nan"))
+    sp.MatmulEx(A.m, False, Bd.m, False, C)
+    _equal(got, want, "dsd after fault")
+    assert sp.pair_errors() == 0
+
+
+def test_graph_capture_with_pairs():
+    """A stream whose pair workspace already exists is captured into a
+    graph: pairs are off inside the capture, so replays (here on the
+    capturing stream and interleaved with eager calls that do use pairs)
+    stay exact."""
+    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
+                                    "f16", seed=6)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        sp.MatmulEx(A.m, False, Bd.m, False, C)  # creates s's workspace
+    torch.cuda.current_stream().wait_stream(s)
+    _equal(got, want, "eager on s")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+    for _ in range(3):
+        got.fill_(float("nan"))
+        g.replay()
+        _equal(got, want, "graph replay")
+        got.fill_(float("nan"))
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+        _equal(got, want, "eager between replays")
+    assert sp.pair_errors() == 0

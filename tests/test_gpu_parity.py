@@ -234,32 +234,6 @@ def test_graph_replay():
         assert torch.equal(c_t, first)
 
 
-@pytest.mark.parametrize("density", [0.1, 0.3, 0.5, 0.9])
-def test_dsd_baseline_config_sampled(density):
-    """BASELINE config 2 (M=K=N=4096) at its four densities: full GPU result,
-    oracle on 3 sampled block-rows (first, middle, last) + row-sum checksum
-    over all rows (linearity: C·1 = A·(B·1))."""
-    rng = np.random.default_rng(7)
-    nz = mu.nonzeros_for_density(4096, 4096, density)
-    A = H.HostSparse(4096, 4096, nz, rng)
-    B = H.HostDense(4096, 4096, rng)
-    C, c_t = H.empty_dense(4096, 4096)
-    sp.Matmul(A.matrix, False, B.matrix, False, C)
-    _sync()
-    gpu = c_t.float().cpu().numpy()
-    dense_a = A.dense()
-    for r in (0, 15, 31):
-        rows = slice(r * 128, (r + 1) * 128)
-        ref = O.gemm(dense_a[rows], False, B.values, False,
-                     a_mask=A.mask()[r:r + 1], threads=H.oracle_threads())
-        H.assert_close(gpu[rows], ref, "f16", f"row-block {r}")
-    ones = B.values.astype(np.float64).sum(axis=1)
-    checksum = dense_a.astype(np.float64) @ ones
-    got = gpu.astype(np.float64).sum(axis=1)
-    scale = np.sqrt(np.mean(checksum ** 2))
-    assert np.abs(got - checksum).max() <= 2e-2 * scale + 1e-2 * np.abs(checksum).max()
-
-
 # --------------------------------------------------------------------- DDS --
 
 def run_dds(p, dtype="f16", seed=0, ex=False):
@@ -420,124 +394,6 @@ def test_sdd_grouped_tiles(k, dtype):
             gpu, ref = run_sdd(p, dtype=dtype, seed=k + 2 * ta + tb)
             H.assert_close(gpu, ref, dtype, f"sdd-grouped {ta}{tb} k={k}")
 
-
-def test_sdd_dds_pair_config3():
-    """BASELINE config 3 (MegaBlocks fwd/bwd pair at 4096^3, 20%), sampled."""
-    rng = np.random.default_rng(11)
-    nz = mu.nonzeros_for_density(4096, 4096, 0.2)
-    x = H.HostDense(4096, 4096, rng)
-    w = H.HostDense(4096, 4096, rng)
-    Cs = H.HostSparse(4096, 4096, nz, rng)
-    sp.AllocateRowIndicesBuffer(Cs.matrix)
-    sp.RowIndices(Cs.matrix, Cs.matrix.row_indices)
-    sp.Matmul(x.matrix, False, w.matrix, False, Cs.matrix)      # SDD
-    g = H.HostDense(4096, 4096, rng)
-    sp.AllocateTransposeBuffers(Cs.matrix)
-    out, out_t = H.empty_dense(4096, 4096)
-    sp.Matmul(g.matrix, False, Cs.matrix, False, out)            # DDS
-    _sync()
-    blocks = Cs.dev_values.float().cpu().numpy()
-    rows = np.repeat(np.arange(32), np.diff(Cs.offsets))
-    for b in (0, len(rows) // 2, len(rows) - 1):
-        r, c = rows[b], Cs.indices[b]
-        ref = O.gemm(x.values[r * 128:(r + 1) * 128], False,
-                     w.values[:, c * 128:(c + 1) * 128], False)
-        H.assert_close(blocks[b], ref, "f16", f"sdd block {b}")
-    # DDS against the oracle on the SDD output as produced (rounded to fp16).
-    sdd_dense = mu.to_dense(4096, 4096, Cs.offsets, Cs.indices, blocks)
-    for r in (0, 17, 31):
-        ref = O.gemm(g.values[r * 128:(r + 1) * 128], False, sdd_dense, False,
-                     b_mask=Cs.mask(), threads=H.oracle_threads())
-        H.assert_close(out_t[r * 128:(r + 1) * 128].float().cpu().numpy(),
-                       ref, "f16", f"dds row-block {r}")
-
-
-
-def test_moe_config4_bf16_sampled():
-    """BASELINE config 4 at full size (8 experts, 8192 tokens, d_model 4096,
-    d_ff 14336, bf16, expert block-diagonal topology): SDD h = x.w1 at the
-    expert blocks, then DSD y = h.w2. Sampled blocks / row-blocks against the
-    oracle; host operands are drawn on the device and only the slices the
-    oracle needs come back."""
-    E, T, DM, FF = 8, 8192, 4096, 14336
-    cols = E * FF
-    rpe, cpe = T // E // 128, FF // 128
-    off, idx = mu.expert_block_diagonal(E, rpe, cpe)
-    nb = int(off[-1])
-    g = torch.Generator(device="cuda")
-    g.manual_seed(4)
-    rnd = lambda *s: (torch.rand(*s, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
-    x, w1, w2 = rnd(T, DM), rnd(DM, cols), rnd(cols, DM)
-    hv = torch.full((nb, 128, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
-    Hm = sp.BlockMatrix(T, cols, 128, nb * 16384, hv,
-                        torch.from_numpy(off).cuda(),
-                        torch.from_numpy(idx.astype(np.int16)).cuda())
-    sp.AllocateRowIndicesBuffer(Hm)
-    sp.RowIndices(Hm, Hm.row_indices)
-    y = torch.full((T, DM), float("nan"), dtype=torch.bfloat16, device="cuda")
-    sp.Matmul(sp.Matrix(T, DM, x), False, sp.Matrix(DM, cols, w1), False, Hm)
-    sp.Matmul(Hm, False, sp.Matrix(cols, DM, w2), False, sp.Matrix(T, DM, y))
-    _sync()
-    f = lambda t: t.float().cpu().numpy()
-    rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
-    for b in (0, 1000, nb // 2 + 37, nb - 1):
-        r, c = int(rows[b]), int(idx[b])
-        ref = O.gemm(f(x[r * 128:(r + 1) * 128]), False,
-                     f(w1[:, c * 128:(c + 1) * 128]), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(hv[b]), ref, "bf16", f"moe sdd block {b}")
-    for r in (0, 29, 63):
-        e = r // rpe
-        h_row = f(hv[off[r]:off[r + 1]]).transpose(1, 0, 2).reshape(128, FF)
-        ref = O.gemm(h_row, False, f(w2[e * FF:(e + 1) * FF]), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(y[r * 128:(r + 1) * 128]), ref, "bf16",
-                       f"moe dsd row-block {r}")
-
-
-def test_tall_panel_config5_sampled():
-    """BASELINE config 5 at full size on one device: DSD M=131072, K=N=4096,
-    2% density (656 blocks over 1024 block-rows, most rows empty). Empty
-    block-rows must be exact zeros; sampled non-empty rows against the
-    oracle; and the per-rank row-panel split (shard_rows_by_nnz) run as
-    separate calls reproduces the single-call result bit-exactly."""
-    rng = np.random.default_rng(5)
-    M = 131072
-    nz = mu.nonzeros_for_density(M, 4096, 0.02)
-    A = H.HostSparse(M, 4096, nz, rng)
-    B = H.HostDense(4096, 4096, rng)
-    C, c_t = H.empty_dense(M, 4096)
-    sp.Matmul(A.matrix, False, B.matrix, False, C)
-    _sync()
-    counts = np.diff(A.offsets)
-    empty = np.nonzero(counts == 0)[0]
-    assert len(empty) > 0
-    e_rows = torch.from_numpy(empty).cuda()
-    blk = c_t.view(M // 128, 128, 4096)
-    assert int(torch.count_nonzero(blk[e_rows])) == 0
-    nonempty = np.nonzero(counts)[0]
-    for r in (nonempty[0], nonempty[len(nonempty) // 2], nonempty[-1]):
-        o0, o1 = A.offsets[r], A.offsets[r + 1]
-        a_row = mu.to_dense(128, 4096, np.array([0, o1 - o0], np.int32),
-                            A.indices[o0:o1], A.values[o0:o1])
-        ref = O.gemm(a_row, False, B.values, False, threads=H.oracle_threads())
-        H.assert_close(c_t[r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
-                       "f16", f"panel row-block {r}")
-    # Row panels as 8 ranks would run them: same bits.
-    for r0, r1 in mu.shard_rows_by_nnz(A.offsets, 8):
-        if r1 == r0:
-            continue
-        po, pi, pv = mu.slice_block_rows(A.offsets, A.indices, A.values, r0, r1)
-        nbp = len(pi)
-        Pm = sp.BlockMatrix((r1 - r0) * 128, 4096, 128, nbp * 16384,
-                            A.dev_values[A.offsets[r0]:A.offsets[r1]]
-                            if nbp else A.dev_values,
-                            torch.from_numpy(po).cuda(),
-                            torch.from_numpy(pi.astype(np.int16)).cuda())
-        Cp, cp_t = H.empty_dense((r1 - r0) * 128, 4096)
-        sp.Matmul(Pm, False, B.matrix, False, Cp)
-        _sync()
-        assert torch.equal(cp_t, c_t[r0 * 128:r1 * 128])
 
 @pytest.mark.parametrize("op", ["dsd", "dds"])
 @pytest.mark.parametrize("ta", [False, True])
@@ -787,7 +643,10 @@ def _device_topology(offsets, indices, rows_b, cols_b):
 
 @pytest.mark.parametrize("shape", [(3, 4, 6), (1, 1, 1), (32, 32, 512),
                                    (64, 896, 7168), (1024, 32, 656),
-                                   (5, 9, 0), (16, 300, 2000), (40, 40, 1600)])
+                                   (5, 9, 0), (16, 300, 2000), (40, 40, 1600),
+                                   # several column slices per launch
+                                   (2000, 2500, 20000), (4100, 5000, 9000),
+                                   (1, 3000, 1500), (3000, 1, 1000)])
 @pytest.mark.parametrize("unordered", [False, True])
 def test_transpose_bit_exact(shape, unordered):
     rows_b, cols_b, nb = shape
@@ -814,6 +673,32 @@ def test_transpose_survey_known_answer():
     assert a.offsets_t.cpu().tolist() == [0, 1, 3, 4, 6]
     assert a.indices_t.cpu().tolist() == [1, 0, 2, 1, 0, 1]
     assert a.block_offsets.cpu().tolist() == [3, 0, 5, 2, 1, 4]
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 6), (32, 32, 512), (1024, 32, 656),
+                                   (64, 896, 7168), (7, 3, 0), (3, 200, 300)])
+@pytest.mark.parametrize("trans", [False, True])
+def test_bitmask_bit_exact(shape, trans):
+    """Bitmask (reference bitmask.cu:7-45) against the oracle's restatement,
+    in both orientations (transposed when offsets_t is set)."""
+    rows_b, cols_b, nb = shape
+    rng = np.random.default_rng(nb + 2 * rows_b)
+    off, idx = mu.random_topology(rows_b, cols_b, nb, rng, unordered=True)
+    a = _device_topology(off, idx, rows_b, cols_b)
+    if trans:
+        sp.AllocateTransposeBuffers(a)
+        sp.Transpose(a)
+    sp.AllocateBitmaskBuffers(a)
+    a.bitmask.fill_(-1)  # every bit must be written
+    sp.Bitmask(a)
+    _sync()
+    if trans:
+        ot, it, _ = O.transpose(off, idx, cols_b)
+        want = O.bitmask(ot, it, rows_b)
+    else:
+        want = O.bitmask(off, idx, cols_b)
+    got = a.bitmask.cpu().numpy().view(np.uint64)[:want.size]
+    assert np.array_equal(got.reshape(want.shape), want)
 
 
 @pytest.mark.parametrize("shape", [(3, 4, 6), (32, 32, 512), (1024, 32, 656),

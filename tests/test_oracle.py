@@ -134,3 +134,19 @@ def test_golden_vectors():
         got = O.gemm(g[p + "/a"], case["ta"], g[p + "/b"], case["tb"],
                      a_mask=a_mask)
         assert np.array_equal(got, g[p + "/c"]), p
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 6), (5, 130, 200), (64, 64, 1000)])
+def test_bitmask_matches_numpy(shape):
+    """oracle_bitmask (bitmask.cu:31-39, bit_matrix.h layout) against an
+    independent numpy packing of the block mask."""
+    rows, cols, nb = shape
+    rng = np.random.default_rng(rows * 7 + cols)
+    off, idx = mu.random_topology(rows, cols, nb, rng, unordered=True)
+    got = O.bitmask(off, idx, cols)
+    mask = mu.block_mask(off, idx, cols).astype(bool)
+    words = (cols + 63) // 64
+    want = np.zeros((rows, words), dtype=np.uint64)
+    for j in range(cols):
+        want[:, j // 64] |= mask[:, j].astype(np.uint64) << np.uint64(j % 64)
+    assert np.array_equal(got, want)
