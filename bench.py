@@ -4,26 +4,39 @@
 Metric: effective TFLOP/s (nnz-FLOPs, 2 * nnz_elements * N per DSD call,
 reference sputnik/block/dsd/dsd_benchmark.cu:113-114) of DSD, block 128,
 M=K=N=4096, fp16 in / fp32 accumulate / fp16 out, at density 0.5 (the
-north-star point); densities 0.1/0.3/0.5/0.9 are reported in "by_density".
+north-star point); densities 0.1/0.3/0.5/0.9 are reported in "by_density",
+each with its own roofline (MFMA- or HBM-bound by arithmetic intensity).
 
 One step = one sputnik_dsd_ex call (C-ABI; NN, so no metadata work) over one
 synthetic BCSR matrix already resident in HBM. Protocol as the reference
 benchmark (dsd_benchmark.cu:82-107): 50 ms idle, W warm-up calls, K timed
-calls between events; barrier + synchronize on both sides; max over ranks.
+calls between HIP events on the launch stream; barrier + synchronize on both
+sides; max over ranks.
 
-Multi-GPU (`--gpus N`, launched by torch.distributed.run): weak scaling by
-row panels — every rank owns a 4096-row panel of an (N*4096) x 4096 BCSR
-matrix (its own random topology) and a replicated B; no collective on the hot
-path. value = nnz-FLOPs of all ranks / max-rank time.
+Multi-GPU (`--gpus N`, launched by torch.distributed.run): one BCSR matrix of
+N x 4096 rows (the same topology on every rank, from a shared seed) is split
+with the library's own
+shard_rows_by_nnz / slice_block_rows; every rank runs its row
+panel against a replicated B; no collective on the hot path. Weak scaling:
+value = nnz-FLOPs of all ranks / max-rank time.
 
-Extra JSON objects: "roofline" (dominant kernel vs the MFMA/HBM peak),
-"cpu_baseline" (the CPU oracle, timed on a bounded sample on rank 0 at N=1).
+Other workloads (`--workload`): sdd_dds (config 3), moe (config 4), panel
+(config 5: M=131072 split over the ranks, strong scaling), op (one product
+and transpose: --op dsd|dds|sdd --trans NN|NT|TN|TT, --api ex|matmul; with
+matmul the device Transpose runs inside every DSD TN/TT and DDS NN/TN step)
+and transpose (the device Transpose alone).
+
+Extra JSON objects: "roofline" (dominant kernel vs its MFMA or HBM roof),
+"cpu_baseline" (the CPU oracle on a bounded sample, 1 thread and all
+allotted threads, rank 0 at N=1), "config1" (BASELINE config 1: the host
+reference matmul at 512^3, 50%), "build" (library source hash vs the tree).
 """
 
 import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -33,8 +46,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_MFMA_TFLOPS = 2500.0  # fp16/bf16 dense, MI355X_MICROARCH.md
-PEAK_HBM_GBS = 8000.0      # HBM3E spec
+PEAK_HBM_GBS = 8000.0      # HBM3E spec, MI355X_MICROARCH.md
+RIDGE = PEAK_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # 312.5 FLOP/B
 BLOCK = 128
+METRIC = ("effective TFLOP/s (nnz-FLOPs) DSD block=128 M=K=N=4096 "
+          "@ 1/2/4/8 GPU vs density")
 
 
 def parse():
@@ -45,9 +61,14 @@ def parse():
                     help="untimed calls first; >= ~10 ms of work so the clock "
                          "has settled (the reference used 10 short calls)")
     ap.add_argument("--workload", default="dsd",
-                    choices=["dsd", "sdd_dds", "moe", "panel"],
+                    choices=["dsd", "sdd_dds", "moe", "panel", "op",
+                             "transpose"],
                     help="dsd: the headline metric (BASELINE config 2); "
-                         "sdd_dds: config 3; moe: config 4; panel: config 5")
+                         "sdd_dds: config 3; moe: config 4; panel: config 5; "
+                         "op: one product/transpose; transpose: metadata")
+    ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"])
+    ap.add_argument("--trans", default="NN", choices=["NN", "NT", "TN", "TT"])
+    ap.add_argument("--api", default="ex", choices=["ex", "matmul"])
     ap.add_argument("--m", type=int, default=4096, help="rows per rank")
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--n", type=int, default=4096)
@@ -56,64 +77,175 @@ def parse():
                     help="densities for by_density ('' to skip)")
     ap.add_argument("--dtype", default="f16", choices=["f16", "bf16"])
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="per CPU-baseline leg (two legs)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) on a node; gloo only for tests that "
+                         "run several ranks on one device")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
-                    help="HBM traffic per launch measured by rocprofv3 --pmc")
+                    help="HBM traffic per launch measured by rocprofv3 --pmc "
+                         "(scripts/pmc.sh), keyed by shape and build hash")
     return ap.parse_args()
 
 
-class Problem:
-    """One rank's DSD operands on the device (+ host copies for the CPU leg)."""
+# ------------------------------------------------------------------ build --
 
-    def __init__(self, m, k, n, density, dtype, seed, device):
+def check_build():
+    """The library's compiled-in source hash against the tree bench.py runs
+    in; a stale library is rebuilt (hipcc is on the GPU box too)."""
+    from sputnik_amd import srchash
+    want = srchash.source_hash()
+    import sputnik_amd as sp
+    got = sp.build_hash() if os.path.exists(sp.LIB_PATH) else None
+    rebuilt = False
+    if got != want:
+        print(f"bench: libsputnik.so built from {got}, tree is {want}: "
+              "rebuilding", file=sys.stderr)
+        subprocess.run(["make", "-s", "-j", "16", "-C",
+                        os.path.join(ROOT, "sputnik_amd")], check=True)
+        rebuilt = True
+        # A fresh process loads the rebuilt library; this one reports it.
+        got = subprocess.run(
+            [sys.executable, "-c",
+             "import sputnik_amd as s; print(s.build_hash())"],
+            capture_output=True, text=True, cwd=ROOT).stdout.strip()
+        if got == want:
+            raise SystemExit(subprocess.call([sys.executable] + sys.argv))
+    return {"hash": got, "source_hash": want, "matches_source": got == want,
+            "rebuilt": rebuilt}
+
+
+# -------------------------------------------------------------- roofline --
+
+def roofline(flops, nbytes, seconds, kernel, traffic=None):
+    """Algorithmic FLOPs / bytes of one launch over its measured duration,
+    against the roof its arithmetic intensity selects."""
+    ai = flops / nbytes
+    tflops = flops / seconds / 1e12
+    gbs = nbytes / seconds / 1e9
+    if ai >= RIDGE:
+        bound, achieved, peak, unit = "mfma", tflops, PEAK_MFMA_TFLOPS, "TFLOP/s"
+    else:
+        bound, achieved, peak, unit = "hbm", gbs, PEAK_HBM_GBS, "GB/s"
+    return {
+        "bound": bound, "achieved": round(achieved, 2), "peak": peak,
+        "unit": unit, "frac": round(achieved / peak, 4), "traffic": traffic,
+        "arithmetic_intensity": round(ai, 1),
+        "tflops": round(tflops, 2),
+        "mfma_frac": round(tflops / PEAK_MFMA_TFLOPS, 4),
+        "algorithmic_GBps": round(gbs, 1),
+        "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+        "algorithmic_flops": flops, "algorithmic_bytes": nbytes,
+        "kernel": kernel,
+    }
+
+
+def pmc_traffic(path, key, build_hash):
+    """HBM bytes per launch from the PMC summary, only when it was measured
+    on this exact build (scripts/pmc.sh writes the build hash)."""
+    if not os.path.exists(path):
+        return None, "no PMC summary"
+    try:
+        with open(path) as f:
+            entry = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None, "unreadable PMC summary"
+    if not entry:
+        return None, f"no PMC entry for {key}"
+    if entry.get("build_hash") != build_hash:
+        return None, (f"PMC entry measured on build {entry.get('build_hash')}, "
+                      f"not {build_hash}")
+    return entry.get("hbm_bytes_per_launch"), "rocprofv3 --pmc, same build"
+
+
+# --------------------------------------------------------------- problems --
+
+def _values(n, td, gen, device):
+    import torch
+    return (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
+
+
+def _td(dtype):
+    import torch
+    return torch.float16 if dtype == "f16" else torch.bfloat16
+
+
+class DsdProblem:
+    """One rank's DSD (op(A) sparse, op(B) dense) on the device, on an
+    explicit topology of op(A)'s storage: A is stored [rows, cols] blocks."""
+
+    def __init__(self, rows, cols, offsets, indices, n, ta, tb, dtype, seed,
+                 device, api="ex"):
         import torch
         import sputnik_amd as sp
-        from sputnik_amd import matrix_utils as mu
-
-        rng = np.random.default_rng(seed)
-        nz = mu.nonzeros_for_density(m, k, density)
-        self.nb = nz // (BLOCK * BLOCK)
-        self.m, self.k, self.n = m, k, n
-        self.offsets, self.indices = mu.random_topology(
-            m // BLOCK, k // BLOCK, self.nb, rng)
-        td = torch.float16 if dtype == "f16" else torch.bfloat16
-        # Values drawn on the device (U(-1,1)); only topology comes from host.
+        self.nb = int(offsets[-1])
+        nz = self.nb * BLOCK * BLOCK
+        self.rows, self.cols, self.n = rows, cols, n
+        self.offsets, self.indices = offsets, indices
+        m, k = (cols, rows) if ta else (rows, cols)
+        self.m, self.k, self.ta, self.tb, self.api = m, k, ta, tb, api
+        td = _td(dtype)
         gen = torch.Generator(device=device)
         gen.manual_seed(seed)
-        self.a_vals = (torch.rand(self.nb * BLOCK * BLOCK, generator=gen,
-                                  device=device) * 2 - 1).to(td)
-        self.b_vals = (torch.rand(k * n, generator=gen, device=device) * 2 - 1
-                       ).to(td)
+        self.a_vals = _values(max(nz, 1), td, gen, device)
+        self.b_vals = _values(k * n, td, gen, device)
         self.c_vals = torch.empty(m * n, dtype=td, device=device)
         self.A = sp.BlockMatrix(
-            m, k, 128, nz, self.a_vals,
-            torch.from_numpy(self.offsets).to(device),
-            torch.from_numpy(self.indices.astype(np.int16)).to(device))
-        self.B = sp.Matrix(k, n, self.b_vals)
+            rows, cols, 128, nz, self.a_vals,
+            torch.from_numpy(np.asarray(offsets, np.int32)).to(device),
+            torch.from_numpy(np.asarray(indices).astype(np.int16)).to(device))
+        if ta:
+            sp.AllocateTransposeBuffers(self.A)
+            sp.Transpose(self.A)
+        self.B = sp.Matrix(*((n, k) if tb else (k, n)), self.b_vals)
         self.C = sp.Matrix(m, n, self.c_vals)
         self.flops = 2.0 * nz * n
-        # Algorithmic HBM bytes of one call: sparse values + metadata +
-        # dense B + dense C (SURVEY §8(d)).
-        self.bytes = nz * 2 + (m // BLOCK + 1) * 4 + self.nb * 2 + k * n * 2 + m * n * 2
+        # Algorithmic HBM bytes of one call: sparse values + metadata (+ the
+        # transposed metadata read in column order) + dense B + dense C.
+        meta = (rows // BLOCK + 1) * 4 + self.nb * 2
+        if ta:
+            meta = (cols // BLOCK + 1) * 4 + self.nb * (2 + 4)
+        self.bytes = nz * 2 + meta + k * n * 2 + m * n * 2
         self.dtype_code = 0 if dtype == "f16" else 1
+        self.kernel = (f"block_gemm_kernel<{dtype}, DSD {'T' if ta else 'N'}"
+                       f"{'T' if tb else 'N'}, 128x512 staggered tile>")
 
     def launcher(self):
         import torch
         import sputnik_amd as sp
-
         L = sp.lib()
         ca, cb, cc = self.A._c(), self.B._c(), self.C._c()
         stream = torch.cuda.current_stream().cuda_stream
-        fn = L.sputnik_dsd_ex
-        args = (ctypes.byref(ca), 0, ctypes.byref(cb), 0, ctypes.byref(cc),
-                self.dtype_code, stream)
+        fn = L.sputnik_dsd_ex if self.api == "ex" else L.sputnik_dsd
+        args = (ctypes.byref(ca), int(self.ta), ctypes.byref(cb), int(self.tb),
+                ctypes.byref(cc), self.dtype_code, stream)
         code = fn(*args)
         if code != 0:
-            raise RuntimeError(f"sputnik_dsd_ex returned {code}")
+            raise RuntimeError(f"dsd returned {code}")
         self._keep = (ca, cb, cc)
         return lambda: fn(*args)
 
+
+def dsd_panel(args, world, rank, device, density, m_total=None, seed_off=0):
+    """The rank's row panel of one (world x m)-row BCSR matrix (or m_total
+    rows), split by nnz with the library's sharding helpers."""
+    from sputnik_amd import matrix_utils as mu
+    rows_total = m_total if m_total is not None else args.m * world
+    nz = mu.nonzeros_for_density(rows_total, args.k, density)
+    rng = np.random.default_rng(args.seed * 7919 + seed_off)  # shared seed
+    off, idx = mu.random_topology(rows_total // BLOCK, args.k // BLOCK,
+                                  nz // (BLOCK * BLOCK), rng)
+    r0, r1 = mu.shard_rows_by_nnz(off, world)[rank]
+    po, pi, _ = mu.slice_block_rows(off, idx, np.zeros(len(idx)), r0, r1)
+    prob = DsdProblem((r1 - r0) * BLOCK, args.k, po, pi, args.n, False, False,
+                      args.dtype, args.seed * 7919 + rank, device)
+    prob.panel = (r0, r1)
+    prob.total_nb = int(off[-1])
+    return prob
+
+
+# ------------------------------------------------------------------ timing --
 
 def barrier(world):
     if world > 1:
@@ -130,6 +262,8 @@ def time_steps(fn, steps, warmup, world):
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    # Events on the launch stream (the library launches on torch's current
+    # stream, which is what the launchers pass).
     start = torch.cuda.Event(enable_timing=True)
     end = torch.cuda.Event(enable_timing=True)
     start.record()
@@ -142,59 +276,131 @@ def time_steps(fn, steps, warmup, world):
     return start.elapsed_time(end)  # ms, this rank
 
 
-def max_over_ranks(x, world):
+def _reduce(x, world, op):
     if world == 1:
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=op)
     return float(t.item())
 
 
-def cpu_baseline(prob: Problem, budget_s: float):
-    """The CPU oracle (reference host matmul restated, zero blocks skipped)
-    on a bounded sample of the same DSD: the first block-rows of A, all of N."""
-    import torch
+def max_over_ranks(x, world):
+    import torch.distributed as dist
+    return _reduce(x, world, dist.ReduceOp.MAX if world > 1 else None)
+
+
+def sum_over_ranks(x, world):
+    import torch.distributed as dist
+    return _reduce(x, world, dist.ReduceOp.SUM if world > 1 else None)
+
+
+# ------------------------------------------------------------ CPU baseline --
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def allotted_threads():
+    """Threads the box allots this process: OMP_NUM_THREADS when set (16 on
+    the GPU pool), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(prob, budget_s):
+    """The CPU oracle (the reference's host matmul restated, zero blocks
+    skipped) on a bounded sample of the same DSD — the leading block-rows of
+    A against all of B — on 1 thread and on every allotted thread."""
     from oracle import oracle as O
     from sputnik_amd import matrix_utils as mu
 
-    threads = max(1, min(16, os.cpu_count() or 1))
     b = prob.b_vals.float().cpu().numpy().reshape(prob.k, prob.n)
     a_vals = prob.a_vals.float().cpu().numpy().reshape(-1, BLOCK, BLOCK)
     mask = mu.block_mask(prob.offsets, prob.indices, prob.k // BLOCK)
+    rows_b = prob.m // BLOCK
 
-    def run(r0, r1):
+    def run(r0, r1, threads):
         o0, o1 = prob.offsets[r0], prob.offsets[r1]
         sub_off = prob.offsets[r0:r1 + 1] - o0
         dense = mu.to_dense((r1 - r0) * BLOCK, prob.k, sub_off,
                             prob.indices[o0:o1], a_vals[o0:o1])
         t0 = time.perf_counter()
         O.gemm(dense, False, b, False, a_mask=mask[r0:r1], threads=threads)
-        dt = time.perf_counter() - t0
-        return dt, 2.0 * (o1 - o0) * BLOCK * BLOCK * prob.n
+        return time.perf_counter() - t0, 2.0 * (o1 - o0) * BLOCK * BLOCK * prob.n
 
-    rows = max(1, min(threads, prob.m // BLOCK))
-    dt, fl = run(0, rows)
-    # Scale the sample to roughly the budget (at least the probe itself).
-    per_row = dt / rows
-    more = int(max(0.0, budget_s - dt) / max(per_row, 1e-9))
-    r1 = min(prob.m // BLOCK, rows + more)
-    total_dt, total_fl = dt, fl
-    if r1 > rows:
-        d2, f2 = run(rows, r1)
-        total_dt += d2
-        total_fl += f2
+    def leg(threads):
+        probe = max(1, min(threads, rows_b))
+        dt, fl = run(0, probe, threads)
+        per_row = dt / probe
+        more = int(max(0.0, budget_s - dt) / max(per_row, 1e-9))
+        more = (more // threads) * threads if threads > 1 else more
+        r1 = min(rows_b, probe + more)
+        if r1 > probe:
+            d2, f2 = run(probe, r1, threads)
+            dt, fl = dt + d2, fl + f2
+        return {"value": round(fl / dt / 1e12, 6), "unit": "TFLOP/s",
+                "cores": threads, "seconds": round(dt, 2),
+                "gflop": round(fl / 1e9, 2), "block_rows": r1}
+
+    threads = allotted_threads()
+    single = leg(1)
+    multi = leg(threads) if threads > 1 else single
     return {
-        "value": total_fl / total_dt / 1e12,
-        "unit": "TFLOP/s",
-        "cores": threads,
+        "value": multi["value"], "unit": "TFLOP/s", "cores": threads,
         "kind": "port",
-        "sample": (f"DSD block-rows 0..{r1 - 1} of {prob.m // BLOCK} "
-                   f"(x all N={prob.n}), {total_fl / 1e9:.2f} nnz-GFLOP in "
-                   f"{total_dt:.1f} s, oracle/oracle.c oracle_gemm with "
-                   f"OpenMP over rows, fp32 in / double acc"),
+        "sample": (f"DSD block-rows 0..{multi['block_rows'] - 1} of {rows_b} "
+                   f"(x all N={prob.n}) of the timed problem, "
+                   f"{multi['gflop']} nnz-GFLOP in {multi['seconds']} s on "
+                   f"{threads} threads; oracle/oracle.c oracle_gemm "
+                   "(Matrix::operator*, matrix_utils.h:376-391, zero blocks "
+                   "skipped), fp32 in / double accumulate"),
+        "single_core": single,
+        "all_cores": multi,
+        "nproc": os.cpu_count(),
+        "threads_allotted": threads,
+        "cpu_model": cpu_model(),
     }
+
+
+def config1_host_reference():
+    """BASELINE config 1: DSD block=128 M=K=N=512, 50% density, fp32, the
+    reference's host path exactly (ToMatrix dense expansion, then the naive
+    Matrix::operator*: no zero-block skip), 1 thread."""
+    from oracle import oracle as O
+    from sputnik_amd import matrix_utils as mu
+    rng = np.random.default_rng(1)
+    nz = mu.nonzeros_for_density(512, 512, 0.5)
+    off, idx = mu.random_topology(4, 4, nz // (BLOCK * BLOCK), rng)
+    vals = mu.random_values((len(idx), BLOCK, BLOCK), rng)
+    b = mu.random_values((512, 512), rng)
+    t0 = time.perf_counter()
+    dense = O.bcsr_to_dense(512, 512, off, idx, vals)
+    O.gemm(dense, False, b, False, threads=1)
+    dt = time.perf_counter() - t0
+    flops = 2.0 * nz * 512
+    return {"metric": "effective GFLOP/s (nnz-FLOPs) DSD block=128 "
+                      "M=K=N=512 50% fp32, host reference",
+            "value": round(flops / dt / 1e9, 4), "unit": "GFLOP/s",
+            "ms": round(dt * 1e3, 2), "cores": 1, "kind": "port",
+            "cpu_model": cpu_model()}
+
+
+# --------------------------------------------------- other workloads ------
 
 class PairProblem:
     """BASELINE config 3: MegaBlocks forward/backward pair at 4096^3, 20%:
@@ -210,11 +416,11 @@ class PairProblem:
         nz = mu.nonzeros_for_density(dim, dim, density)
         nb = nz // (BLOCK * BLOCK)
         off, idx = mu.random_topology(dim // BLOCK, dim // BLOCK, nb, rng)
-        td = torch.float16 if dtype == "f16" else torch.bfloat16
+        td = _td(dtype)
         gen = torch.Generator(device=device)
         gen.manual_seed(seed)
-        rnd = lambda n: (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
-        self.x, self.w, self.g = rnd(dim * dim), rnd(dim * dim), rnd(dim * dim)
+        self.x, self.w, self.g = (_values(dim * dim, td, gen, device)
+                                  for _ in range(3))
         self.out = torch.empty(dim * dim, dtype=td, device=device)
         self.cv = torch.empty(nz, dtype=td, device=device)
         self.C = sp.BlockMatrix(dim, dim, 128, nz, self.cv,
@@ -226,6 +432,7 @@ class PairProblem:
         sp.Transpose(self.C)
         self.dim, self.nb = dim, nb
         self.flops = 2.0 * nz * dim * 2
+        self.bytes = 2 * (nz * 2 + 2 * dim * dim * 2) + nb * 8
         self.dtype_code = 0 if dtype == "f16" else 1
         self.desc = (f"SDD(x,w)->C then DDS(g,C) block=128 M=K=N={dim} "
                      f"density={density} {dtype} (MatmulEx metadata)")
@@ -262,13 +469,12 @@ class MoeProblem:
         nb = int(off[-1])
         nz = nb * BLOCK * BLOCK
         cols = experts * d_ff
-        td = torch.float16 if dtype == "f16" else torch.bfloat16
+        td = _td(dtype)
         gen = torch.Generator(device=device)
         gen.manual_seed(seed)
-        rnd = lambda n: (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
-        self.x = rnd(tokens * d_model)
-        self.w1 = rnd(d_model * cols)
-        self.w2 = rnd(cols * d_model)
+        self.x = _values(tokens * d_model, td, gen, device)
+        self.w1 = _values(d_model * cols, td, gen, device)
+        self.w2 = _values(cols * d_model, td, gen, device)
         self.y = torch.empty(tokens * d_model, dtype=td, device=device)
         self.hv = torch.empty(nz, dtype=td, device=device)
         self.H = sp.BlockMatrix(tokens, cols, 128, nz, self.hv,
@@ -278,6 +484,8 @@ class MoeProblem:
         sp.RowIndices(self.H, self.H.row_indices)
         self.dims = (tokens, d_model, cols)
         self.flops = 2.0 * nz * d_model * 2
+        self.bytes = (2 * nz * 2 + tokens * d_model * 2 * 2 +
+                      2 * d_model * cols * 2)
         self.dtype_code = 0 if dtype == "f16" else 1
         self.dtype_name = dtype
         self.desc = (f"MoE {experts} experts tokens={tokens} d_model={d_model} "
@@ -301,39 +509,169 @@ class MoeProblem:
         return lambda: (L.sputnik_sdd(*a1), L.sputnik_dsd_ex(*a2))
 
 
-def run_other(args, world, rank, device):
-    """Non-headline BASELINE configs: one JSON line each (same contract)."""
-    import torch
+class OpProblem:
+    """One product with one transpose combination at M=K=N (4096, density
+    as given): DSD / DDS through MatmulEx (metadata precomputed) or Matmul
+    (the device Transpose inside every step where the sparse operand is read
+    in column order: DSD TN/TT, DDS NN/TN), or SDD (no metadata)."""
+
+    def __init__(self, args, device):
+        import torch
+        import sputnik_amd as sp
+        from sputnik_amd import matrix_utils as mu
+        d, dens, op = args.k, args.density, args.op
+        ta, tb = args.trans[0] == "T", args.trans[1] == "T"
+        rng = np.random.default_rng(args.seed)
+        nz = mu.nonzeros_for_density(d, d, dens)
+        nb = nz // (BLOCK * BLOCK)
+        off, idx = mu.random_topology(d // BLOCK, d // BLOCK, nb, rng)
+        td = _td(args.dtype)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(args.seed)
+        self.sv = _values(nz, td, gen, device)
+        self.x = _values(d * d, td, gen, device)
+        self.out = torch.empty(d * d, dtype=td, device=device)
+        self.S = sp.BlockMatrix(d, d, 128, nz, self.sv,
+                                torch.from_numpy(off).to(device),
+                                torch.from_numpy(idx.astype(np.int16)).to(device))
+        sp.AllocateTransposeBuffers(self.S)
+        sp.Transpose(self.S)
+        self.S.create_metadata = args.api == "matmul"
+        if op == "sdd":
+            self.y = _values(d * d, td, gen, device)
+            sp.AllocateRowIndicesBuffer(self.S)
+            sp.RowIndices(self.S, self.S.row_indices)
+        self.op, self.ta, self.tb, self.api = op, ta, tb, args.api
+        self.flops = 2.0 * nz * d
+        meta_t = (op == "dsd" and ta) or (op == "dds" and not tb)
+        meta = (d // BLOCK + 1) * 4 + nb * (6 if meta_t else 2)
+        self.bytes = (nz * 2 + meta + d * d * 2 * (2 if op == "sdd" else 1) +
+                      (0 if op == "sdd" else d * d * 2))
+        self.dtype_code = 0 if args.dtype == "f16" else 1
+        self.meta_t = meta_t
+        self.desc = (f"{op.upper()} {args.trans} block=128 M=K=N={d} "
+                     f"density={dens} {args.dtype} "
+                     f"({'MatmulEx' if args.api == 'ex' else 'Matmul'}"
+                     f"{', device Transpose in every step' if meta_t and args.api == 'matmul' else ''})")
+        self.kernel = f"block_gemm_kernel<{args.dtype}, {op.upper()} {args.trans}>"
+
+    def launcher(self):
+        import torch
+        import sputnik_amd as sp
+        L = sp.lib()
+        d = self.k = self.dim = int(self.S.rows)
+        cS = self.S._c()
+        cx = sp.Matrix(d, d, self.x)._c()
+        co = sp.Matrix(d, d, self.out)._c()
+        stream = torch.cuda.current_stream().cuda_stream
+        ta, tb, code = int(self.ta), int(self.tb), self.dtype_code
+        if self.op == "dsd":
+            fn = L.sputnik_dsd_ex if self.api == "ex" else L.sputnik_dsd
+            a = (ctypes.byref(cS), ta, ctypes.byref(cx), tb, ctypes.byref(co), code, stream)
+        elif self.op == "dds":
+            fn = L.sputnik_dds_ex if self.api == "ex" else L.sputnik_dds
+            a = (ctypes.byref(cx), ta, ctypes.byref(cS), tb, ctypes.byref(co), code, stream)
+        else:
+            cy = sp.Matrix(d, d, self.y)._c()
+            fn = L.sputnik_sdd
+            a = (ctypes.byref(cx), ta, ctypes.byref(cy), tb, ctypes.byref(cS), code, stream)
+            self._y = cy
+        assert fn(*a) == 0
+        self._keep = (cS, cx, co)
+        return lambda: fn(*a)
+
+
+class TransposeProblem:
+    """The device Transpose alone on the headline topology (4096^2 blocks at
+    the given density): offsets_t / indices_t / block_offsets."""
+
+    def __init__(self, args, device):
+        import torch
+        import sputnik_amd as sp
+        from sputnik_amd import matrix_utils as mu
+        d = args.k
+        rng = np.random.default_rng(args.seed)
+        nz = mu.nonzeros_for_density(d, d, args.density)
+        nb = nz // (BLOCK * BLOCK)
+        off, idx = mu.random_topology(d // BLOCK, d // BLOCK, nb, rng)
+        self.S = sp.BlockMatrix(d, d, 128, nz,
+                                torch.empty(1, dtype=torch.float16, device=device),
+                                torch.from_numpy(off).to(device),
+                                torch.from_numpy(idx.astype(np.int16)).to(device))
+        sp.AllocateTransposeBuffers(self.S)
+        self.flops = 0.0
+        self.bytes = (d // BLOCK + 1) * 4 * 2 + nb * (2 + 2 + 4)
+        self.desc = f"Transpose block=128 {d}x{d} density={args.density} ({nb} blocks)"
+
+    def launcher(self):
+        import torch
+        import sputnik_amd as sp
+        L = sp.lib()
+        c = self.S._c()
+        stream = torch.cuda.current_stream().cuda_stream
+        assert L.sputnik_transpose(ctypes.byref(c), stream) == 0
+        self._keep = c
+        return lambda: L.sputnik_transpose(ctypes.byref(c), stream)
+
+
+def emit(line):
+    print(json.dumps(line))
+    sys.stdout.flush()
+
+
+def run_other(args, world, rank, device, build):
+    """Non-headline workloads: one JSON line each (same contract)."""
+    scaling = "weak"
     if args.workload == "sdd_dds":
         prob = PairProblem(args.k, 0.2, args.dtype, args.seed * 7919 + rank, device)
         metric = "effective TFLOP/s (nnz-FLOPs) SDD+DDS pair block=128 M=K=N=4096 20%"
     elif args.workload == "moe":
         prob = MoeProblem("bf16", args.seed * 7919 + rank, device)
         metric = "effective TFLOP/s (nnz-FLOPs) MoE SDD+DSD 8 experts bf16"
+    elif args.workload == "op":
+        prob = OpProblem(args, device)
+        metric = (f"effective TFLOP/s (nnz-FLOPs) {args.op.upper()} {args.trans} "
+                  f"block=128 M=K=N={args.k} {args.density}")
+    elif args.workload == "transpose":
+        prob = TransposeProblem(args, device)
+        metric = "microseconds per device Transpose (BCSR metadata)"
     else:  # panel: config 5, M=131072 total, row panels over ranks
-        m_rank = 131072 // world
-        prob = Problem(m_rank, 4096, 4096, 0.02, args.dtype,
-                       args.seed * 7919 + rank, device)
-        prob.desc = (f"DSD block=128 M=131072 (/{world} ranks = {m_rank}) K=N=4096 "
-                     f"density=0.02 {args.dtype}")
+        prob = dsd_panel(args, world, rank, device, 0.02, m_total=131072,
+                         seed_off=5)
+        r0, r1 = prob.panel
+        prob.desc = (f"DSD block=128 M=131072 K=N=4096 density=0.02 "
+                     f"{args.dtype}, rank {rank} block-rows {r0}..{r1 - 1} "
+                     f"of 1024 (shard_rows_by_nnz over {world})")
         metric = "effective TFLOP/s (nnz-FLOPs) row-panel DSD M=131072 K=N=4096 2%"
+        scaling = "strong"
     fn = prob.launcher()
     ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
     per = ms / args.steps
-    tflops = prob.flops * world / (per * 1e-3) / 1e12
+    flops_all = sum_over_ranks(prob.flops, world)
     extra = {}
+    if args.workload == "transpose":
+        value, unit, hib = per * 1e3, "us", False
+    else:
+        value, unit, hib = flops_all / (per * 1e-3) / 1e12, "TFLOP/s", True
+        extra["roofline"] = roofline(prob.flops, prob.bytes, per * 1e-3,
+                                     getattr(prob, "kernel", "block_gemm_kernel"))
     if args.workload == "panel" and world > 1:
         # Optional gather of the dense result (config 5): reported beside the
-        # hot path, never inside it.
+        # hot path, never inside it. Equal-size panels of the padded maximum.
+        import torch
         import torch.distributed as dist
-        full = torch.empty(world * prob.c_vals.numel(), dtype=prob.c_vals.dtype,
-                           device=device)
-        dist.all_gather_into_tensor(full, prob.c_vals)
+        rows = torch.tensor([prob.C.rows], device=device)
+        dist.all_reduce(rows, op=dist.ReduceOp.MAX)
+        pad = torch.zeros(int(rows.item()) * args.n, dtype=prob.c_vals.dtype,
+                          device=device)
+        pad[:prob.c_vals.numel()] = prob.c_vals
+        full = torch.empty(world * pad.numel(), dtype=pad.dtype, device=device)
+        dist.all_gather_into_tensor(full, pad)
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
         for _ in range(5):
-            dist.all_gather_into_tensor(full, prob.c_vals)
+            dist.all_gather_into_tensor(full, pad)
         torch.cuda.synchronize()
         ag = max_over_ranks((time.perf_counter() - t0) / 5 * 1e3, world)
         extra["allgather_ms"] = round(ag, 4)
@@ -341,15 +679,14 @@ def run_other(args, world, rank, device):
             full.numel() * full.element_size() * (world - 1) / world / (ag * 1e-3) / 1e9, 1)
         del full
     if rank == 0:
-        print(json.dumps({**extra,
-            "metric": metric, "value": round(tflops, 2), "unit": "TFLOP/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(per, 5), "higher_is_better": True,
-            "scaling": "weak" if args.workload != "panel" else "strong",
-            "vs_baseline": None,
-            "dtype": getattr(prob, "dtype_name", args.dtype),
-            "data": "synthetic", "config": {"workload": prob.desc},
-        }))
+        emit({**extra,
+              "metric": metric, "value": round(value, 3), "unit": unit,
+              "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+              "ms_per_step": round(per, 5), "higher_is_better": hib,
+              "scaling": scaling, "vs_baseline": None,
+              "dtype": getattr(prob, "dtype_name", args.dtype),
+              "data": "synthetic", "config": {"workload": prob.desc},
+              "build": build})
 
 
 def main():
@@ -360,16 +697,27 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}",
               file=sys.stderr)
+    build = check_build() if rank == 0 else None
 
     import torch
+    # One rank per GPU; the modulo only matters for tests that put several
+    # (gloo) ranks on a one-GPU box.
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+        barrier(world)  # every rank sees local rank 0's (re)built library
+    if build is None:
+        import sputnik_amd as sp
+        build = {"hash": sp.build_hash()}
 
     if args.workload != "dsd":
-        run_other(args, world, rank, device)
+        run_other(args, world, rank, device, build)
         if world > 1:
             import torch.distributed as dist
             dist.destroy_process_group()
@@ -381,55 +729,39 @@ def main():
     results = {}
     head = None
     for d in densities:
-        prob = Problem(args.m, args.k, args.n, d, args.dtype,
-                       args.seed * 7919 + rank, device)
+        prob = dsd_panel(args, world, rank, device, d)
         fn = prob.launcher()
-        ms = time_steps(fn, args.steps, args.warmup, world)
-        ms = max_over_ranks(ms, world)
+        ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
         per_step = ms / args.steps
-        tflops = prob.flops * world / (per_step * 1e-3) / 1e12
+        flops_all = sum_over_ranks(prob.flops, world)
+        tflops = flops_all / (per_step * 1e-3) / 1e12
+        key = f"dsd_{prob.m}x{args.k}x{args.n}_{d}_{args.dtype}"
+        traffic, note = pmc_traffic(args.pmc, key, build.get("hash"))
+        roof = roofline(prob.flops, prob.bytes, per_step * 1e-3, prob.kernel,
+                        traffic)
+        roof["traffic_source"] = note
         results[d] = {"value": round(tflops, 2), "ms_per_step": round(per_step, 5),
-                      "nnz_blocks_per_rank": prob.nb}
+                      "nnz_blocks_per_rank": prob.nb, "roofline": roof}
         if head is None:
-            head = (prob, per_step, tflops)
+            head = (prob, per_step, tflops, roof)
         else:
             del prob
         torch.cuda.empty_cache()
 
-    prob, per_step, tflops = head
-    # Dominant (only) kernel of a step: block_gemm DSD NN. One launch per
+    # Dominant (only) kernel of a step: block_gemm DSD NN, one launch per
     # step, so the event-timed average over the K launches is its duration.
-    kernel_s = per_step * 1e-3
-    achieved = prob.flops / kernel_s / 1e12
-    traffic = None
-    if os.path.exists(args.pmc):
-        try:
-            with open(args.pmc) as f:
-                pmc = json.load(f)
-            key = f"dsd_{args.m}x{args.k}x{args.n}_{args.density}_{args.dtype}"
-            traffic = pmc.get(key, {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
-    roofline = {
-        "bound": "mfma",
-        "achieved": round(achieved, 2),
-        "peak": PEAK_MFMA_TFLOPS,
-        "unit": "TFLOP/s",
-        "frac": round(achieved / PEAK_MFMA_TFLOPS, 4),
-        "traffic": traffic,
-        "kernel": "block_gemm_kernel<f16, DSD NN, CfgWide8S: 128x512 tile, staggered>",
-        "algorithmic_bytes": prob.bytes,
-        "algorithmic_flops": prob.flops,
-    }
+    prob, per_step, tflops, roof = head
 
     cpu = None
+    config1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(prob, args.cpu_seconds)
+        config1 = config1_host_reference()
 
     if rank == 0:
-        line = {
-            "metric": "effective TFLOP/s (nnz-FLOPs) DSD block=128 M=K=N=4096 "
-                      "@ 1/2/4/8 GPU vs density",
+        r0, r1 = prob.panel
+        emit({
+            "metric": METRIC,
             "value": round(tflops, 2),
             "unit": "TFLOP/s",
             "n_gpus": world,
@@ -447,13 +779,17 @@ def main():
                             f"{args.dtype} (NN, MatmulEx)",
                 "block": 128, "m_per_rank": args.m, "k": args.k, "n": args.n,
                 "density": args.density,
-                "parallelism": f"row-panel x{world}, no collective",
+                "parallelism": (f"row panels of one {args.m * world}-row "
+                                f"matrix split by nnz over {world} rank(s) "
+                                f"(rank 0: block-rows {r0}..{r1 - 1}), "
+                                "no collective"),
             },
             "by_density": {str(k): v for k, v in results.items()},
-            "roofline": roofline,
+            "roofline": roof,
             "cpu_baseline": cpu,
-        }
-        print(json.dumps(line))
+            "config1": config1,
+            "build": build,
+        })
 
     if world > 1:
         import torch.distributed as dist

@@ -208,7 +208,7 @@ int sputnik_transpose(const sputnik_block_matrix_t *a, void *stream) {
 int sputnik_bitmask(const sputnik_block_matrix_t *m, void *stream) {
   if (!m || !m->bitmask) return hipErrorInvalidValue;
   const bool trans = m->offsets_t != nullptr;
-  if ((trans ? !m->indices_t : !m->offsets) ||
+  if ((trans ? !m->offsets_t : !m->offsets) ||
       (m->nonzeros > 0 && !(trans ? m->indices_t : m->indices)))
     return hipErrorInvalidValue;
   if (m->block_size != 128 && m->block_size != 64 && m->block_size != 32 &&

@@ -205,3 +205,88 @@ def test_two_rank_gloo_sharded_dds_and_sdd_match_unsharded(tmp_path):
     want = np.stack([full[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128]
                      for r, c in zip(ri, idx)])
     assert np.array_equal(got["sdd"], want)
+
+
+# ---- the same splits on the GPU: each rank runs the HIP kernel -------------
+# World size 2 with the gloo backend; both ranks share the box's one device
+# (the 8-GPU node is the driver's). Integer operand values make every split
+# exact, so the gathered panels must equal the unsharded launch bit for bit.
+
+def _int_problem(seed=21):
+    rng = np.random.default_rng(seed)
+    R, C, N = 24, 16, 1024
+    off, idx = mu.random_topology(R, C, 190, rng, unordered=True)
+    vals = rng.integers(-1, 2, size=(190, 128, 128)).astype(np.float32)
+    b = rng.integers(-1, 2, size=(C * 128, N)).astype(np.float32)
+    return R, C, N, off, idx, vals, b
+
+
+def _hip_dsd(off, idx, vals, rows_b, cols_b, b):
+    import sputnik_amd as sp
+    dev = torch.device("cuda", 0)
+    nb = len(idx)
+    A = sp.BlockMatrix(rows_b * 128, cols_b * 128, 128, nb * 16384,
+                       torch.from_numpy(vals).half().to(dev),
+                       torch.from_numpy(off.astype(np.int32)).to(dev),
+                       torch.from_numpy(idx.astype(np.int16)).to(dev))
+    bt = torch.from_numpy(b).half().to(dev)
+    c = torch.full((rows_b * 128, b.shape[1]), float("nan"),
+                   dtype=torch.float16, device=dev)
+    sp.Matmul(A, False, sp.Matrix(*b.shape, bt),
+              False, sp.Matrix(rows_b * 128, b.shape[1], c))
+    torch.cuda.synchronize()
+    return c.float().cpu().numpy()
+
+
+def _worker_hip(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    R, C, N, off, idx, vals, b = _int_problem()
+    r0, r1 = mu.shard_rows_by_nnz(off, world)[rank]
+    p_off, p_idx, p_vals = mu.slice_block_rows(off, idx, vals, r0, r1)
+    panel = (_hip_dsd(p_off, p_idx, p_vals, r1 - r0, C, b) if r1 > r0
+             else np.zeros((0, N), np.float32))
+    full = np.concatenate(_gather_equal(panel, world))
+    if rank == 0:
+        np.save(out_path, full)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_sharded_hip_dsd_matches_unsharded(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = str(tmp_path / "c.npy")
+    mp.spawn(_worker_hip, args=(2, _free_port(), out), nprocs=2, join=True)
+    R, C, N, off, idx, vals, b = _int_problem()
+    whole = _hip_dsd(off, idx, vals, R, C, b)
+    exact = mu.to_dense(R * 128, C * 128, off, idx, vals).astype(np.float64) @ b
+    got = np.load(out)
+    assert np.array_equal(got, whole)
+    assert np.array_equal(got, exact)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_shard_one_matrix():
+    """bench.py's N>1 path (one matrix split by shard_rows_by_nnz, max over
+    ranks, whole-job value) on two ranks sharing the device, gloo backend."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--sweep", "",
+           "--no-cpu", "--dist-backend", "gloo"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                         cwd=root)
+    assert res.returncode == 0, res.stderr[-2000:]
+    line = json.loads([x for x in res.stdout.splitlines()
+                       if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert "split by nnz over 2" in line["config"]["parallelism"]
