@@ -697,9 +697,11 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}",
               file=sys.stderr)
+    # torch first: it loads its HIP runtime, which libsputnik.so then shares
+    # (loading the library first would bring in a second runtime).
+    import torch
     build = check_build() if rank == 0 else None
 
-    import torch
     # One rank per GPU; the modulo only matters for tests that put several
     # (gloo) ranks on a one-GPU box.
     local = local % max(1, torch.cuda.device_count())

@@ -138,6 +138,13 @@ def lib() -> ctypes.CDLL:
                 f"{LIB_PATH} is missing: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` or "
                 "`make -C sputnik_amd`. There is no CPU fallback.")
+        # PyTorch ships its own HIP runtime (same soname as ROCm's). Load it
+        # first so the library binds to that one copy; loading libsputnik.so
+        # first would pull in /opt/rocm's runtime next to torch's.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         handle = ctypes.CDLL(LIB_PATH)
         for name, args in _SIGNATURES.items():
             fn = getattr(handle, name)
