@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--ldpad", type=int, default=0,
+                    help="experiment builds: pad B's row stride by this many "
+                         "bytes (SPUTNIK_AMD_EXP_LDPAD; B reallocated)")
     ap.add_argument("--op", default="dsd", choices=["dsd", "sdd", "moe_sdd", "moe_dsd"])
     args = ap.parse_args()
     import torch
@@ -30,7 +33,20 @@ def main():
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     if args.op == "dsd":
-        prob = bench.Problem(args.m, args.k, args.n, args.density, args.dtype, 0, dev)
+        import numpy as np
+        from sputnik_amd import matrix_utils as mu
+        nz = mu.nonzeros_for_density(args.m, args.k, args.density)
+        off, idx = mu.random_topology(args.m // 128, args.k // 128,
+                                      nz // (128 * 128),
+                                      np.random.default_rng(0))
+        prob = bench.DsdProblem(args.m, args.k, off, idx, args.n, False,
+                                False, args.dtype, 0, dev)
+        if args.ldpad:
+            os.environ["SPUTNIK_AMD_EXP_LDPAD"] = str(args.ldpad)
+            import torch as _t
+            prob.b_vals = _t.zeros(args.k * args.n + args.k * args.ldpad // 2,
+                                   dtype=prob.b_vals.dtype, device=dev)
+            prob.B.data = prob.b_vals
         ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
         fname = "sputnik_dsd_ex"
     elif args.op == "sdd":

@@ -94,7 +94,8 @@ static bool PairsEnabled() {
 #endif
 static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair = 0;
-  if (!CfgSparse::kStagger || CfgSparse::kWGs != 1) return;
+  if (!(CfgSparse::kStagger || CfgSparse::kFlat) || CfgSparse::kWGs != 1)
+    return;
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -239,6 +240,10 @@ Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
       ta ? static_cast<const int *>(a.block_offsets) : nullptr;
   p->d_data = static_cast<const char *>(b.data);
   p->d_ld = (long long)s.ldb * 2;
+#if SPUTNIK_EXP != 0
+  // Experiment builds only: pad B's row stride (the caller allocates it).
+  if (const char *e = std::getenv("SPUTNIK_AMD_EXP_LDPAD")) p->d_ld += std::atoi(e);
+#endif
   p->c_data = static_cast<char *>(c.data);
   p->c_ld = (long long)s.ldc * 2;
   p->num_rows = s.m / kBM;
