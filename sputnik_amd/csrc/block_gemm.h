@@ -300,6 +300,18 @@ __device__ __forceinline__ v4u rsrc_words(const char *base) {
   return r;
 }
 
+template <int N>
+constexpr int kMf_check() { return N; }
+
+// Descriptor of an empty buffer (num_records 0): every lane is out of range,
+// so an LDS-DMA from it writes zeros and moves no memory.
+__device__ __forceinline__ v4u rsrc_words_or_empty(const char *base,
+                                                   bool valid) {
+  v4u r = rsrc_words(base);
+  r[2] = ((SPUTNIK_EXP & 16384) != 0 || valid) ? kNumRecords : 0u;
+  return r;
+}
+
 // One 1 KiB LDS-DMA piece: 16 bytes per lane from r + voffset to LDS
 // [lds_addr + 16 * lane]. M0 (the LDS base) is compiler-reserved, so it is
 // saved and restored inside the statement; SALU M0 write -> LDS-DMA needs one
@@ -350,6 +362,7 @@ struct TileConfig {
   // two waves of a SIMD cover each other's memory issue with MFMAs instead
   // of alternating whole phases.
   static constexpr bool kFlat = FLAT_ != 0;
+  static constexpr bool kSplit = FLAT_ == 2;
 };
 
 // 8 waves, 64x64 each, BK=64, one workgroup per CU (first-generation DSD/DDS).
@@ -373,6 +386,10 @@ using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
 // The same tile and ring on the flat interleaved pipeline.
 using CfgWide8F = TileConfig<512, 2, 4, 32, 4, 1, 0, 1, 1>;
+// Flat pipeline with split DMA roles (pipeline_split): waves 0-3 stream the
+// dense operand two steps ahead, waves 4-7 the sparse blocks about six steps
+// ahead (their reads go beyond L2), each with its own vmcnt.
+using CfgWide8P = TileConfig<512, 2, 4, 32, 4, 1, 0, 1, 2>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 // SDD, one block per workgroup with K split inside it: 8 waves in two
@@ -1191,6 +1208,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     s16x4 blo[kFN], bhi[kFN];
   };
   auto pipeline_flat = [&](int e0, int nblk, int flush_blk) {
+   if constexpr (Cfg::kFlat && !Cfg::kSplit) {
     if (nblk <= 0) return;
     auto entry = [&](int x) {
       return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
@@ -1480,6 +1498,406 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         pad_acc();
       }
     }
+   }
+  };
+
+  // ---- DSD / DDS, flat pipeline with split DMA roles (Cfg::kSplit) -------
+  // The sparse blocks S come from beyond L2 (every XCD reads all of them
+  // once), the dense panel D mostly from L2, and a wave's vmcnt retires its
+  // DMA in issue order, so one wave cannot keep S far ahead while waiting on
+  // D. Waves 0-3 (one per SIMD) therefore issue only D, two steps ahead, into
+  // a 3-slot ring; waves 4-7 only S, in full 128-byte lines, 5-6 steps ahead,
+  // into a 4-slot ring of two-step images; every wave computes its 64 x 128
+  // sub-tile from both rings. LDS: [S ring 4 x 16 KiB][D ring 3 x 32 KiB].
+  // Steps past the row's end issue out-of-range DMA (zeros, no memory
+  // traffic) so every wait count is a constant.
+  //  - D: step j issues D(j + 3) into slot j % 3 (held D(j), read in step
+  //    j - 1); before step j a D-wave needs D(j + 1): vmcnt(8).
+  //  - S: step j issues half (j + 1) & 1 of image v = (j + 1) / 2 + 3 into
+  //    slot v % 4 (held v - 4, last read in step 2v - 8 < j); before step j
+  //    an S-wave needs image (j + 1) / 2: vmcnt(10) for even j, 8 for odd.
+  auto pipeline_split = [&](int e0, int nblk, int flush_blk) {
+   if constexpr (Cfg::kSplit) {
+    if (nblk <= 0) return;
+    constexpr int kSImg = 2 * kSBytes;       // S image: two steps, 16 KiB
+    constexpr int kSRing = 4 * kSImg;
+    constexpr int kDPieces = kDBytes / 1024 / (kNW / 2);  // per D-wave
+    constexpr int kSPieces = kSImg / 1024 / (kNW / 2);    // per S-wave, image
+    constexpr int kSImgRow = kSKC ? 128 : kBM * 2;         // S image row bytes
+    static_assert(kSRing + 3 * kDBytes <= kRingBytes && kDPieces == 8 &&
+                      kSPieces == 4 && kMf_check<kFM * kFN>() == 32,
+                  "split pipeline geometry");
+    const bool dwave = wave < kNW / 2;
+    const int rw = dwave ? wave : wave - kNW / 2;  // index inside the role
+    auto entry = [&](int x) {
+      return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
+    };
+    // (k-block, storage block) of blocks b .. b + 3 (b + 3 prefetched).
+    int k0 = 0, k1 = 0, k2 = 0, k3 = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    auto load_e = [&](int x, int &kk, int &ss) {
+      const int ge = entry(e0 + min(x, nblk - 1));
+      kk = scalar_load_short(p.s_indices, ge);
+      ss = p.s_block_offsets != nullptr ? scalar_load_int(p.s_block_offsets, ge)
+                                        : ge;
+    };
+    // Per-lane DMA offsets: D-waves 8 pieces of a D image, S-waves 4 of an
+    // S image (2 per step).
+    uint32_t voff[kDPieces];
+#pragma unroll
+    for (int q = 0; q < kDPieces; ++q) {
+      uint32_t off = 0;
+      if (dwave) {
+        const int g = rw * kDPieces + q;
+        bool ok;
+        if constexpr (kDKC) {
+          const int jj = kKcRowsPerInstr * g + lane / kKcChunks;
+          const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(jj);
+          off = (uint32_t)(jj * p.d_ld + c * 16);
+          ok = j0 + jj < p.j_limit;
+        } else {
+          const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
+          const int pc = lane % kDChunksPerRow;
+          const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
+          off = (uint32_t)(k * p.d_ld + c * 16);
+          ok = j0 + c * 8 < p.j_limit;
+        }
+        if (!ok) off = kOOB;
+      } else if (q < kSPieces) {
+        const int g = rw * kSPieces + q;
+        if constexpr (kSKC) {  // [128 rows][64 k]: 8 rows of 128 B a piece
+          const int row = 8 * g + lane / 8;
+          const int c = (lane % 8) ^ kc_key<8>(row);
+          off = (uint32_t)(row * 256 + c * 16);
+        } else {  // [64 k][128 m]: 4 rows of 256 B a piece
+          const int k = 4 * g + lane / 16;
+          const int pc = lane % 16;
+          const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
+          off = (uint32_t)(k * 256 + c * 16);
+        }
+      }
+      voff[q] = off;
+    }
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(
+        (__attribute__((address_space(3))) char *)(lds));
+    const uint32_t lds_s = lds0, lds_d = lds0 + kSRing;
+    // Base of D image (block with k-block kb, quarter q); of S image (block
+    // with storage block sb, k-half dq).
+    auto d_src = [&](int kb, int q) -> const char * {
+      const long long kg = (long long)kb * kBlock + q * kBK;
+      return kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
+                  : p.d_data + kg * p.d_ld + (long long)j0 * 2;
+    };
+    auto s_src = [&](int sb, int dq) -> const char * {
+      return p.s_data + (long long)sb * (kBlock * kBlock * 2) +
+             (kSKC ? dq * 128 : dq * (64 * 256));
+    };
+    // Read offsets (as pipeline_flat; the S image rows are 128 B when
+    // k-contiguous, with 8 chunks, and kk selects the step's k-half).
+    auto kc_off_s = [&](int kk) -> uint32_t {
+      const int row = row_w + (lane & 15);
+      const int c = 4 * kk + (lane >> 4);
+      return (uint32_t)(row * 128 + ((c ^ kc_key<8>(row)) << 4));
+    };
+    auto mn_off = [&](int col0, int row_bytes, int kk) -> uint32_t {
+      const int q = (lane >> 2) & 3, pp = lane & 3, g = lane >> 4;
+      const int k = 32 * kk + 8 * g + q;
+      return (uint32_t)(k * row_bytes + (pp << 3) +
+                        (((col0 >> 4) ^ tr_key(k)) << 5));
+    };
+    auto kc_off_d = [&](int row0) -> uint32_t {
+      const int row = row0 + (lane & 15);
+      const int c = lane >> 4;
+      return (uint32_t)(row * kKcRow + ((c ^ kc_key<kBK / 8>(row)) << 4));
+    };
+    const uint32_t a_l0 = kSKC ? kc_off_s(0) : mn_off(row_w, kSImgRow, 0);
+    const uint32_t a_l1 = kSKC ? kc_off_s(1) : mn_off(row_w, kSImgRow, 1);
+    const uint32_t b_l = kDKC ? kc_off_d(col_w) : mn_off(col_w, kDRowBytes, 0);
+    constexpr int kDImgRow = kDKC ? kKcRow : kDRowBytes;
+    constexpr int kAP = kSKC ? kFM : 2 * kFM;
+    constexpr int kBP = kDKC ? kFN : 2 * kFN;
+    constexpr int kRP = kAP + kBP;
+    constexpr int kMf = kFM * kFN;
+    auto read_piece = [&](auto r_c, FFrags &F, const uint32_t *abase,
+                          const uint32_t *bbase) {
+      constexpr int R = decltype(r_c)::value;
+      if constexpr ((SPUTNIK_EXP & 256) != 0) return;
+      if constexpr (R < kAP) {
+        if constexpr (kSKC) {
+          ds_read128_asm<R * 16 * 128>(F.a[R], abase[0]);
+        } else {
+          constexpr int f = R / 2;
+          if constexpr (R % 2 == 0)
+            ds_read_tr_asm<0>(F.alo[f], abase[f]);
+          else
+            ds_read_tr_asm<4 * kSImgRow>(F.ahi[f], abase[f]);
+        }
+      } else {
+        constexpr int Rb = R - kAP;
+        if constexpr (kDKC) {
+          ds_read128_asm<Rb * 16 * kKcRow>(F.b[Rb], bbase[0]);
+        } else {
+          constexpr int f = Rb / 2;
+          if constexpr (Rb % 2 == 0)
+            ds_read_tr_asm<0>(F.blo[f], bbase[f]);
+          else
+            ds_read_tr_asm<4 * kDImgRow>(F.bhi[f], bbase[f]);
+        }
+      }
+    };
+    // Fragment bases of one step: S image slot / k-half, D slot (opaque, so
+    // no slot's addresses are hoisted out of the loop).
+    auto step_bases = [&](uint32_t s_img, int kk, uint32_t d_img,
+                          uint32_t *abase, uint32_t *bbase) {
+      asm volatile("" : "+s"(s_img), "+s"(d_img));
+      const uint32_t a0 = s_img + (kk ? a_l1 : a_l0), b0 = d_img + b_l;
+#pragma unroll
+      for (int f = 0; f < (kSKC ? 1 : kFM); ++f) abase[f] = a0 ^ (f << 5);
+#pragma unroll
+      for (int f = 0; f < (kDKC ? 1 : kFN); ++f) bbase[f] = b0 ^ (f << 5);
+    };
+    auto fence_frags = [&](FFrags &F) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int f = 0; f < kFM; ++f) {
+        if constexpr (kSKC) asm volatile("" : "+v"(F.a[f]));
+        else asm volatile("" : "+v"(F.alo[f]), "+v"(F.ahi[f]));
+      }
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) {
+        if constexpr (kDKC) asm volatile("" : "+v"(F.b[f]));
+        else asm volatile("" : "+v"(F.blo[f]), "+v"(F.bhi[f]));
+      }
+    };
+    auto fence_acc = [&]() {
+#pragma unroll
+      for (int a = 0; a < kFM; ++a)
+#pragma unroll
+        for (int b = 0; b < kFN; ++b) asm volatile("" : "+v"(acc[a][b]));
+    };
+    auto pad_acc = [&]() {
+      fence_acc();
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+      fence_acc();
+    };
+    auto opnd_a = [&](FFrags &F, int f) -> s16x8 {
+      if constexpr (kSKC) return F.a[f];
+      else return __builtin_shufflevector(F.alo[f], F.ahi[f], 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    auto opnd_b = [&](FFrags &F, int f) -> s16x8 {
+      if constexpr (kDKC) return F.b[f];
+      else return __builtin_shufflevector(F.blo[f], F.bhi[f], 0, 1, 2, 3, 4, 5, 6, 7);
+    };
+    // One role's DMA of a step: the D-waves' 8 pieces or the S-waves' 2
+    // (pieces 2..7 are skipped by a uniform branch).
+    struct Dma { v4u r; uint32_t m0; };
+    auto dma_k = [&](const Dma &d, int k, uint32_t vo) {
+      if constexpr ((SPUTNIK_EXP & 2) != 0) return;
+      if constexpr ((SPUTNIK_EXP & 1024) != 0) { if (!dwave) return; }
+      if constexpr ((SPUTNIK_EXP & 2048) != 0) { if (dwave) return; }
+      dma_asm(d.r, vo, d.m0 + k * 1024);
+    };
+    struct Sched {
+      static constexpr int dma_pos(int k) { return 1 + 4 * k; }  // k < 8
+      static constexpr int read_pos(int r) { return 2 + r * (kMf - 4) / kRP; }
+      static constexpr int dma_at(int m) {
+        for (int k = 0; k < 8; ++k)
+          if (dma_pos(k) == m) return k;
+        return -1;
+      }
+      static constexpr int reads_from(int m) {
+        for (int r = 0; r < kRP; ++r)
+          if (read_pos(r) >= m) return r;
+        return kRP;
+      }
+    };
+    int b = 0;      // current block
+    int dsl = 0;    // D slot of step j (j % 3)
+    // Step H of block b (j = 4b + H).
+    auto sstep = [&](auto h_c, auto last_c, FFrags &cur, FFrags &nxt) {
+      constexpr int H = decltype(h_c)::value;
+      constexpr bool LAST = decltype(last_c)::value;
+      constexpr bool kNext = !(LAST && H == 3);
+      if constexpr (kNext) {
+        if constexpr ((SPUTNIK_EXP & 8192) != 0)
+          wait_vmcnt<0>();
+        else if (dwave) {
+          if constexpr ((SPUTNIK_EXP & 32768) != 0) wait_vmcnt<0>();
+          else wait_vmcnt<8>();
+        } else if constexpr ((SPUTNIK_EXP & 65536) != 0)
+          wait_vmcnt<0>();
+        else if constexpr (H % 2 == 0)
+          wait_vmcnt<10>();
+        else
+          wait_vmcnt<8>();
+        __builtin_amdgcn_s_barrier();
+        if constexpr ((SPUTNIK_EXP & 131072) != 0) {
+          if (!dwave) __builtin_amdgcn_s_sleep(30);
+        }
+        if constexpr ((SPUTNIK_EXP & 262144) != 0) {
+          if (dwave) __builtin_amdgcn_s_sleep(30);
+        }
+      }
+      // This step's DMA (role-selected SGPRs).
+      Dma d;
+      {
+        // D(j + 3): block b, quarter 3 (H = 0) or block b + 1, quarter H - 1.
+        const int dkb = H == 0 ? k0 : k1;
+        const bool dval = H == 0 ? true : b + 1 < nblk;
+        // S: image v = 2b + 3 (H = 0), 2b + 4 (H = 1, 2), 2b + 5 (H = 3);
+        // block v / 2, k-half v % 2, piece half (H + 1) & 1.
+        constexpr int kVoff = H == 0 ? 3 : (H == 3 ? 5 : 4);
+        const int v = 2 * b + kVoff;
+        const int sblk = H == 0 ? s1 : s2;
+        const bool sval = v / 2 < nblk;
+        constexpr int kHalf = (H + 1) & 1;
+        const uint32_t dm0 = lds_d + (uint32_t)(dsl * kDBytes) +
+                             (uint32_t)(rw * kDPieces * 1024);
+        const uint32_t sm0 = lds_s + (uint32_t)((v & 3) * kSImg) +
+                             (uint32_t)((rw * kSPieces + 2 * kHalf) * 1024);
+        const v4u rdv = rsrc_words_or_empty(d_src(dkb, (H + 3) & 3), dval);
+        const v4u rsv = rsrc_words_or_empty(s_src(sblk, kVoff & 1), sval);
+        d.r = dwave ? rdv : rsv;
+        d.m0 = __builtin_amdgcn_readfirstlane(dwave ? dm0 : sm0);
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          d.r[w] = __builtin_amdgcn_readfirstlane(d.r[w]);
+      }
+      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
+      if constexpr (kNext) {
+        // Step j + 1: S image (j + 1) / 2 = 2b + (H + 1) / 2, k-half
+        // (H + 1) & 1; D slot (j + 1) % 3.
+        const int simg = (2 * b + (H + 1) / 2) & 3;
+        const int dnext = dsl == 2 ? 0 : dsl + 1;
+        step_bases(lds_s + (uint32_t)(simg * kSImg), (H + 1) & 1,
+                   lds_d + (uint32_t)(dnext * kDBytes), abase, bbase);
+      }
+      s16x8 ca[kFM], cb[kFN];
+#pragma unroll
+      for (int f = 0; f < kFM; ++f) ca[f] = opnd_a(cur, f);
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) cb[f] = opnd_b(cur, f);
+      static_for<0, kMf>([&](auto m_c) {
+        constexpr int m = decltype(m_c)::value;
+        constexpr int fa = m % kFM, fb = m / kFM;
+        if constexpr ((SPUTNIK_EXP & 1) == 0) {
+          if constexpr (kOutT)
+            mfma_asm<T>(acc[fa][fb], ca[fa], cb[fb]);
+          else
+            mfma_asm<T>(acc[fa][fb], cb[fb], ca[fa]);
+        }
+        // The last step has no barrier, so it issues no DMA: its slots may
+        // still be read by other waves.
+        constexpr int k = kNext ? Sched::dma_at(m) : -1;
+        if constexpr (k >= 0) {
+          if constexpr (k < 2) {
+            // S-waves take the pieces of this step's image half.
+            constexpr int kHalf = (H + 1) & 1;
+            dma_k(d, k, kHalf == 0 ? voff[k]
+                                   : (dwave ? voff[k] : voff[k + 2]));
+          } else {
+            if (dwave) dma_k(d, k, voff[k]);
+          }
+        }
+        constexpr int r0 = Sched::reads_from(m), r1 = Sched::reads_from(m + 1);
+        if constexpr (kNext && r1 > r0) {
+          static_for<r0, r1>([&](auto r_c) { read_piece(r_c, nxt, abase, bbase); });
+        }
+      });
+#pragma unroll
+      for (int f = 0; f < kFM; ++f) asm volatile("" :: "v"(ca[f]));
+#pragma unroll
+      for (int f = 0; f < kFN; ++f) asm volatile("" :: "v"(cb[f]));
+      if constexpr (kNext) fence_frags(nxt);
+      dsl = dsl == 2 ? 0 : dsl + 1;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+
+    // Prologue (after a barrier: the row ranking's per-wave scratch lies in
+    // the ring): D(0..2) and S images 0..2 plus half 0 of image 3, then the
+    // fragments of step 0.
+    FFrags f0, f1;
+    load_e(0, k0, s0);
+    load_e(1, k1, s1);
+    load_e(2, k2, s2);
+    asm volatile("" : "+s"(k0), "+s"(s0), "+s"(k1), "+s"(s1), "+s"(k2),
+                 "+s"(s2));
+    __builtin_amdgcn_s_barrier();
+    {
+      if (dwave) {
+        static_for<0, 3>([&](auto q_c) {
+          constexpr int Q = decltype(q_c)::value;
+          Dma d;
+          d.r = rsrc_words(d_src(k0, Q));
+          d.m0 = __builtin_amdgcn_readfirstlane(
+              lds_d + (uint32_t)(Q * kDBytes + rw * kDPieces * 1024));
+          static_for<0, kDPieces>([&](auto k_c) {
+            constexpr int K = decltype(k_c)::value;
+            dma_k(d, K, voff[K]);
+          });
+        });
+      } else {
+        // Images 0 (block 0, half 0), 1 (block 0, half 1), 2 (block 1, half
+        // 0), and half 0 of image 3 (block 1, half 1).
+        static_for<0, 4>([&](auto v_c) {
+          constexpr int V = decltype(v_c)::value;
+          Dma d;
+          d.r = rsrc_words_or_empty(s_src(V < 2 ? s0 : s1, V & 1),
+                                    V / 2 < nblk);
+          d.m0 = __builtin_amdgcn_readfirstlane(
+              lds_s + (uint32_t)(V * kSImg + rw * kSPieces * 1024));
+          static_for<0, (V < 3 ? kSPieces : 2)>([&](auto k_c) {
+            constexpr int K = decltype(k_c)::value;
+            dma_k(d, K, voff[K]);
+          });
+        });
+      }
+    }
+    load_e(3, k3, s3);
+    if (dwave) wait_vmcnt<16>(); else wait_vmcnt<10>();
+    __builtin_amdgcn_s_barrier();
+    {
+      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
+      step_bases(lds_s, 0, lds_d, abase, bbase);
+      static_for<0, kRP>([&](auto r_c) { read_piece(r_c, f0, abase, bbase); });
+      fence_frags(f0);
+    }
+    pad_acc();
+    auto rotate = [&]() {  // block b + 1 begins: entries move down one
+      asm volatile("" : "+s"(k3), "+s"(s3));
+      k0 = k1; s0 = s1; k1 = k2; s1 = s2; k2 = k3; s2 = s3;
+      load_e(b + 4, k3, s3);  // b is the finished block
+    };
+    for (; b + 1 < nblk; ++b) {
+      sstep(I0{}, std::false_type{}, f0, f1);
+      sstep(I1{}, std::false_type{}, f1, f0);
+      sstep(I2{}, std::false_type{}, f0, f1);
+      sstep(I3{}, std::false_type{}, f1, f0);
+      if constexpr (kPairs) {
+        if (b + 1 == flush_blk) {
+          pad_acc();
+          publish();
+          pad_acc();
+        }
+      }
+      rotate();
+    }
+    sstep(I0{}, std::true_type{}, f0, f1);
+    sstep(I1{}, std::true_type{}, f1, f0);
+    sstep(I2{}, std::true_type{}, f0, f1);
+    sstep(I3{}, std::true_type{}, f1, f0);
+    // Drain the tail's zero-fill DMAs before anything else uses the ring.
+    wait_vmcnt<0>();
+    pad_acc();
+    if constexpr (kPairs) {
+      if (b + 1 == flush_blk) {
+        publish();
+        pad_acc();
+      }
+    }
+   }
   };
 
   // Steps [s_begin, s_end) of sparse block-row `srow` whose entries start at
@@ -1997,7 +2415,10 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
     // needs 12 more address registers than it has and spills; those two
     // keep the per-step pipeline.)
-    if constexpr (Cfg::kFlat)
+    if constexpr (Cfg::kSplit)
+      pipeline_split(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
+                     p_flush > 0 ? p_flush / kStepsPerBlock : -1);
+    else if constexpr (Cfg::kFlat)
       pipeline_flat(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
                     p_flush > 0 ? p_flush / kStepsPerBlock : -1);
     else if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
