@@ -754,6 +754,10 @@ def main():
     # step, so the event-timed average over the K launches is its duration.
     prob, per_step, tflops, roof = head
 
+    anchor = dense_anchor(prob, args, device) if rank == 0 else None
+    if anchor:
+        anchor["dsd_over_dense"] = round(tflops / world / anchor["tflops"], 3)
+
     cpu = None
     config1 = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -788,6 +792,7 @@ def main():
             },
             "by_density": {str(k): v for k, v in results.items()},
             "roofline": roof,
+            "dense_anchor": anchor,
             "cpu_baseline": cpu,
             "config1": config1,
             "build": build,
@@ -796,6 +801,38 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def dense_anchor(prob, args, device, iters=50):
+    """The vendor dense GEMM (torch.matmul -> hipBLASLt) on the same FLOPs:
+    M x N x (K * density), random normal data, timed like the DSD steps. The
+    MFMA peak is a spec number; this is what a dense GEMM reaches on this
+    GPU under the same clocks and power draw."""
+    import torch
+    dt = torch.float16 if args.dtype == "f16" else torch.bfloat16
+    kd = max(BLOCK, int(round(args.k * args.density / BLOCK)) * BLOCK)
+    try:
+        a = torch.randn(args.m, kd, dtype=dt, device=device)
+        b = torch.randn(kd, args.n, dtype=dt, device=device)
+        for _ in range(10):
+            torch.matmul(a, b)
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(5):
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                torch.matmul(a, b)
+            e.record()
+            torch.cuda.synchronize()
+            times.append(s.elapsed_time(e) / iters)
+    except RuntimeError as exc:  # reported, never fatal
+        return {"error": str(exc)[:200]}
+    ms = sorted(times)[len(times) // 2]
+    return {"op": "torch.matmul (hipBLASLt)",
+            "shape": [args.m, args.n, kd], "us": round(ms * 1e3, 2),
+            "tflops": round(2.0 * args.m * args.n * kd / (ms * 1e-3) / 1e12, 1)}
 
 
 if __name__ == "__main__":

@@ -436,7 +436,8 @@ hipError_t BuildTransposed(const BlockMatrix &a, hipStream_t stream) {
   const int b = AsInt(a.block_size);
   if (b == 0) return hipErrorNotSupported;
   return LaunchTransposeMetadata(
-      a.rows / b, a.cols / b, static_cast<const int *>(a.offsets),
+      a.rows / b, a.cols / b, static_cast<int>(a.nonzeros / (b * b)),
+      static_cast<const int *>(a.offsets),
       static_cast<const short *>(a.indices), static_cast<int *>(a.offsets_t),
       static_cast<short *>(a.indices_t), static_cast<int *>(a.block_offsets),
       stream);

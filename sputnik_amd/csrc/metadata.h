@@ -6,7 +6,8 @@
 
 namespace sputnik_amd {
 
-hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
+// blocks: stored blocks (offsets[block_rows], from the matrix's nonzeros).
+hipError_t LaunchTransposeMetadata(int block_rows, int block_cols, int blocks,
                                    const int *offsets, const short *indices,
                                    int *offsets_t, short *indices_t,
                                    int *block_offsets, hipStream_t stream);

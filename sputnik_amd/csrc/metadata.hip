@@ -32,6 +32,8 @@ constexpr int kTransposeWaves = kTransposeThreads / 64;
 constexpr int kMaxBlockCols = 32768;  // int16 block-column indices
 // LDS words (32 rows each) of one slice: bit words + their prefix counts.
 constexpr int kTransposeWords = 16384;
+// Blocks per thread kept in registers by the one-slice path.
+constexpr int kTransposeCache = 4;
 
 // Calls f(row, entry, column) for every stored block of `slice` columns
 // [c0, c1), one wave per block-row.
@@ -51,9 +53,35 @@ __device__ __forceinline__ void for_slice_blocks(int block_rows,
   }
 }
 
+// Exclusive prefix of v over the workgroup's threads (thread order) and the
+// total: wave scans by shuffles, then the wave totals; two barriers.
+__device__ __forceinline__ int block_exclusive_scan(int v, int *wsum,
+                                                    int *total) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int below = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kTransposeWaves; ++i) {
+    const int t = wsum[i];
+    below += i < wave ? t : 0;
+    all += t;
+  }
+  __syncthreads();  // wsum may be reused
+  *total = all;
+  return below + incl - v;
+}
+
 __global__ void __launch_bounds__(kTransposeThreads)
     transpose_metadata_kernel(int block_rows, int block_cols, int slice,
-                              const int *__restrict__ offsets,
+                              int blocks, const int *__restrict__ offsets,
                               const short *__restrict__ indices,
                               int *__restrict__ offsets_t,
                               short *__restrict__ indices_t,
@@ -61,34 +89,65 @@ __global__ void __launch_bounds__(kTransposeThreads)
   __shared__ unsigned bits[kTransposeWords];
   __shared__ int prefix[kTransposeWords];
   __shared__ int partial[kTransposeThreads];
+  __shared__ int wsum[kTransposeWaves];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int words = (block_rows + 31) >> 5;  // per column
   const int c0 = blockIdx.x * slice;
   const int c1 = min(c0 + slice, block_cols);
   const int ncols = c1 - c0;
-  const int blocks = offsets[block_rows];
 
   // 1. Bit matrix of the slice; blocks left of the slice (the slice's base).
-  for (int w = tid; w < ncols * words; w += kTransposeThreads) bits[w] = 0;
-  int left = 0;
-  for (int k = tid; k < blocks; k += kTransposeThreads)
-    left += indices[k] < c0 ? 1 : 0;
-  partial[tid] = left;
-  __syncthreads();
-  for_slice_blocks(block_rows, offsets, indices, c0, c1,
-                   [&](int r, int, int c) {
-                     atomicOr(&bits[(c - c0) * words + (r >> 5)],
-                              1u << (r & 31));
-                   });
-  // Block sum of `left` (tree over partial[]).
-  for (int stride = kTransposeThreads / 2; stride > 0; stride >>= 1) {
+  // Small matrices (one slice, a few blocks per thread) keep each block's
+  // (row, column) in registers: one round trip to memory for the offsets
+  // (staged in `prefix`, free until step 2) and the indices, issued together;
+  // a block's row is a binary search of the staged offsets.
+  const bool cached = gridDim.x == 1 &&
+                      blocks <= kTransposeCache * kTransposeThreads &&
+                      block_rows < kTransposeWords;
+  int crow[kTransposeCache], ccol[kTransposeCache];
+  if (cached) {
+    int *offs = prefix;
+    for (int i = tid; i <= block_rows; i += kTransposeThreads)
+      offs[i] = offsets[i];
+#pragma unroll
+    for (int q = 0; q < kTransposeCache; ++q) {
+      const int k = tid + q * kTransposeThreads;
+      ccol[q] = k < blocks ? indices[k] : -1;
+    }
+    for (int w = tid; w < ncols * words; w += kTransposeThreads) bits[w] = 0;
     __syncthreads();
-    if (tid < stride) partial[tid] += partial[tid + stride];
+#pragma unroll
+    for (int q = 0; q < kTransposeCache; ++q) {
+      const int k = tid + q * kTransposeThreads;
+      if (ccol[q] < 0) continue;
+      int lo = 0, hi = block_rows;  // offs[lo] <= k < offs[hi]
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (offs[mid] <= k) lo = mid; else hi = mid;
+      }
+      crow[q] = lo;
+      atomicOr(&bits[ccol[q] * words + (lo >> 5)], 1u << (lo & 31));
+    }
+  } else {
+    for (int w = tid; w < ncols * words; w += kTransposeThreads) bits[w] = 0;
+    __syncthreads();
+    for_slice_blocks(block_rows, offsets, indices, c0, c1,
+                     [&](int r, int, int c) {
+                       atomicOr(&bits[(c - c0) * words + (r >> 5)],
+                                1u << (r & 31));
+                     });
   }
-  __syncthreads();
-  const int base = partial[0];
-  __syncthreads();
+  // Blocks left of the slice (none for the first slice).
+  int base = 0;
+  if (c0 > 0) {
+    int left = 0;
+    for (int k = tid; k < blocks; k += kTransposeThreads)
+      left += indices[k] < c0 ? 1 : 0;
+    block_exclusive_scan(left, wsum, &base);
+  } else {
+    __syncthreads();
+  }
 
   // 2. Per-column word prefix counts (one wave per column, 64 words a pass)
   //    and column totals.
@@ -114,17 +173,8 @@ __global__ void __launch_bounds__(kTransposeThreads)
   // 3. Exclusive scan of the column totals -> offsets_t (slice <= threads:
   //    thread t owns column c0 + t).
   const int mine = tid < ncols ? partial[tid] : 0;
-  __syncthreads();
-  partial[tid] = mine;
-  __syncthreads();
-  for (int stride = 1; stride < kTransposeThreads; stride <<= 1) {
-    const int v = tid >= stride ? partial[tid - stride] : 0;
-    __syncthreads();
-    partial[tid] += v;
-    __syncthreads();
-  }
-  const int first = base + partial[tid] - mine;
-  __syncthreads();
+  int unused;
+  const int first = base + block_exclusive_scan(mine, wsum, &unused);
   if (tid < ncols) {
     partial[tid] = first;  // first slot of column c0 + tid
     offsets_t[c0 + tid] = first;
@@ -133,16 +183,21 @@ __global__ void __launch_bounds__(kTransposeThreads)
   __syncthreads();
 
   // 4. Scatter: slot = column start + rank of the block-row in its column.
-  for_slice_blocks(block_rows, offsets, indices, c0, c1,
-                   [&](int r, int k, int c) {
-                     const int cl = c - c0;
-                     const int w = cl * words + (r >> 5);
-                     const int rank =
-                         prefix[w] + __popc(bits[w] & ((1u << (r & 31)) - 1u));
-                     const int pos = partial[cl] + rank;
-                     indices_t[pos] = static_cast<short>(r);
-                     block_offsets[pos] = k;
-                   });
+  auto scatter = [&](int r, int k, int c) {
+    const int cl = c - c0;
+    const int w = cl * words + (r >> 5);
+    const int rank = prefix[w] + __popc(bits[w] & ((1u << (r & 31)) - 1u));
+    const int pos = partial[cl] + rank;
+    indices_t[pos] = static_cast<short>(r);
+    block_offsets[pos] = k;
+  };
+  if (cached) {
+#pragma unroll
+    for (int q = 0; q < kTransposeCache; ++q)
+      if (ccol[q] >= 0) scatter(crow[q], tid + q * kTransposeThreads, ccol[q]);
+  } else {
+    for_slice_blocks(block_rows, offsets, indices, c0, c1, scatter);
+  }
 }
 
 // ---- Bitmask (reference sputnik/block/bitmask/bitmask.cu:7-45 with the
@@ -304,7 +359,7 @@ hipError_t LaunchExpertTopology(const int *padded_bins, int num_experts,
   return hipGetLastError();
 }
 
-hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
+hipError_t LaunchTransposeMetadata(int block_rows, int block_cols, int blocks,
                                    const int *offsets, const short *indices,
                                    int *offsets_t, short *indices_t,
                                    int *block_offsets, hipStream_t stream) {
@@ -322,8 +377,8 @@ hipError_t LaunchTransposeMetadata(int block_rows, int block_cols,
   const int grid = (block_cols + slice - 1) / slice;
   hipLaunchKernelGGL(transpose_metadata_kernel, dim3(grid),
                      dim3(kTransposeThreads), 0, stream, block_rows,
-                     block_cols, slice, offsets, indices, offsets_t, indices_t,
-                     block_offsets);
+                     block_cols, slice, blocks, offsets, indices, offsets_t,
+                     indices_t, block_offsets);
   return hipGetLastError();
 }
 
