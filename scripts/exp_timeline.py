@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""Per-workgroup timeline of one block_gemm launch (SPUTNIK_EXP & 512
+builds; SPUTNIK_AMD_LIB selects the library). For each workload: the launch
+span and, over the workgroups, when they started and how long their setup,
+pipeline, pair collect and tile write took (us, 100 MHz clock).
+
+Usage: exp_timeline.py [workload ...]  (dsd10 dsd20 dsd50 dds20 sdd20)"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import sputnik_amd as sp  # noqa: E402
+from sputnik_amd import matrix_utils as mu  # noqa: E402
+
+
+def topo(density, seed=0):
+    nz = mu.nonzeros_for_density(4096, 4096, density)
+    rng = np.random.default_rng(seed)
+    return mu.random_topology(32, 32, nz // (128 * 128), rng)
+
+
+def launcher(name, device):
+    L = sp.lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    if name.startswith("dsd"):
+        off, idx = topo(int(name[3:]) / 100)
+        prob = bench.DsdProblem(4096, 4096, off, idx, 4096, False, False,
+                                "f16", 0, device)
+        return prob, prob.launcher()
+    prob = bench.PairProblem(4096, int(name[3:]) / 100, "f16", 0, device)
+    d = prob.dim
+    cx, cw, cg, co = (sp.Matrix(d, d, t)._c()
+                      for t in (prob.x, prob.w, prob.g, prob.out))
+    cC = prob.C._c()
+    keep = (cx, cw, cg, co, cC)
+    if name.startswith("sdd"):
+        args = (ctypes.byref(cx), 0, ctypes.byref(cw), 0, ctypes.byref(cC), 0,
+                stream)
+        return (prob, keep), lambda: L.sputnik_sdd(*args)
+    args = (ctypes.byref(cg), 0, ctypes.byref(cC), 0, ctypes.byref(co), 0,
+            stream)
+    return (prob, keep), lambda: L.sputnik_dds_ex(*args)
+
+
+def summarize(buf, wgs):
+    t = buf[:wgs * 16].reshape(wgs, 16).astype(np.int64)
+    live = t[:, 0] > 0
+    t = t[live]
+    t[:, 2] = np.where(t[:, 2] == 0, t[:, 3], t[:, 2])  # no pair stamp
+    t0 = t[:, 0].min()
+    us = lambda x: x / 100.0  # noqa: E731  (100 MHz)
+    seg = {
+        "start": us(t[:, 0] - t0),
+        "setup": us(t[:, 1] - t[:, 0]),
+        "pipeline": us(t[:, 2] - t[:, 1]),
+        "collect": us(t[:, 3] - t[:, 2]),
+        "write": us(t[:, 4] - t[:, 3]),
+        "end": us(t[:, 4] - t0),
+    }
+    out = {"workgroups": int(live.sum()), "span_us": float(seg["end"].max())}
+    for k, v in seg.items():
+        out[k] = {"p50": round(float(np.median(v)), 2),
+                  "p90": round(float(np.percentile(v, 90)), 2),
+                  "max": round(float(v.max()), 2)}
+    steps = t[:, 7]
+    role = t[:, 8]
+    prod = role == 1
+    cons = role == 2
+    if cons.any():
+        pub = {int(t[i, 10]): t[i, 5] for i in np.nonzero(prod)[0]}
+        rows = []
+        for i in np.nonzero(cons)[0]:
+            pt = pub.get(int(t[i, 10]))
+            rows.append((us(t[i, 2] - t0), us(pt - t0) if pt else -1,
+                         us(t[i, 6] - t[i, 2]), us(t[i, 3] - t[i, 6])))
+        rows = np.array(rows)
+        out_c = {"pipeline_end": rows[:, 0], "producer_published": rows[:, 1],
+                 "poll": rows[:, 2], "partial_load": rows[:, 3]}
+        out_pairs = {k: {"p50": round(float(np.median(v)), 2),
+                         "max": round(float(v.max()), 2)}
+                     for k, v in out_c.items()}
+        worst = int(np.argmax(rows[:, 0] + rows[:, 2] + rows[:, 3]))
+        out_pairs["worst"] = [round(float(x), 2) for x in rows[worst]]
+    else:
+        out_pairs = None
+    out["steps"] = {"mean": round(float(steps.mean()), 1),
+                    "max": int(steps.max())}
+    out["roles"] = {str(r): int((role == r).sum()) for r in (0, 1, 2)}
+    out["pairs"] = out_pairs
+    slow = int(np.argmax(seg["end"]))
+    out["last_wg"] = {k: round(float(v[slow]), 2) for k, v in seg.items()}
+    out["last_wg"]["steps"] = int(steps[slow])
+    out["last_wg"]["role"] = int(role[slow])
+    return out
+
+
+def main():
+    names = sys.argv[1:] or ["dsd10", "dsd50", "dds20", "sdd20"]
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    L = sp.lib()
+    L.sputnik_exp_set_debug.argtypes = [ctypes.c_void_p]
+    buf = torch.zeros(16 * 8192, dtype=torch.int64, device=device)
+    L.sputnik_exp_set_debug(ctypes.c_void_p(buf.data_ptr()))
+    for name in names:
+        keep, fn = launcher(name, device)
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize()
+        buf.zero_()
+        torch.cuda.synchronize()
+        fn()
+        torch.cuda.synchronize()
+        res = summarize(buf.cpu().numpy(), 8192)
+        res["workload"] = name
+        print(json.dumps(res), flush=True)
+        del keep
+    L.sputnik_exp_set_debug(ctypes.c_void_p(0))
+
+
+if __name__ == "__main__":
+    main()

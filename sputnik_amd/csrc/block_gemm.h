@@ -530,6 +530,17 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // SPUTNIK_EXP & 512: timeline of each workgroup (wave 0; 100 MHz clock):
+  // entry, pipeline start, pipeline end, collect end, tile written, pair
+  // partial published (producer), pair flag seen (consumer).
+  unsigned long long tl_stamp[7] = {};
+  auto tl = [&](int i) {
+    if constexpr ((SPUTNIK_EXP & 512) != 0) {
+      asm volatile("" ::: "memory");
+      tl_stamp[i] = __builtin_amdgcn_s_memrealtime();
+    }
+  };
+  tl(0);
   const int wsub = kKS > 1 ? wave % (Cfg::kWM * kWN) : wave;
   const int wm = wsub / kWN;
   const int wn = wsub % kWN;
@@ -868,6 +879,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       if (wave == kNW - 1 && lane == 0 && !p.pair_fault)
         __hip_atomic_store(p.pair_flags + pair_id, p.pair_epoch,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tl(5);
       zero_acc();
     }
   };
@@ -894,22 +906,47 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
                              __HIP_MEMORY_SCOPE_SYSTEM);
         *ok = got ? 1 : 0;
       }
+      wait_vmcnt<0>();  // no DMA of the pipeline still lands in the ring
       __syncthreads();
+      tl(6);
       const bool got = __builtin_amdgcn_readfirstlane(*ok) != 0;
+      if (!got) {
+        const float nan = __builtin_nanf("");
+#pragma unroll
+        for (int a = 0; a < kFM; ++a)
+#pragma unroll
+          for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{nan, nan, nan, nan};
+        return;
+      }
+      // The partial (sc1, as it was stored) comes in by LDS-DMA, each
+      // wave's fragments into its own LDS region (above the scratch words),
+      // all of a half in flight at once: the accumulators leave no registers
+      // for loads, and register loads issued a few at a time cost one round
+      // trip per few KiB (8.5 us for the 256 KiB tile).
+      constexpr int kFrags = kFM * kFN;
+      constexpr int kHalfFr = kFrags / 2;
+      constexpr int kRegion = kHalfFr * 1024;
+      static_assert(16384 + kNW * kRegion <= kRingBytes && kFrags % 2 == 0,
+                    "pair partial staging fits in the ring");
       const __amdgpu_buffer_rsrc_t rp = pair_rsrc();
       const int lb = pair_lane_base();
-      const float nan = __builtin_nanf("");
+      char *region = lds + 16384 + wave * kRegion;
+      const f32x4 *mine =
+          reinterpret_cast<const f32x4 *>(region) + lane;
 #pragma unroll
-      for (int a = 0; a < kFM; ++a)
+      for (int h = 0; h < 2; ++h) {
 #pragma unroll
-        for (int b = 0; b < kFN; ++b) {
-          if (got)
-            acc[a][b] += __builtin_bit_cast(
-                f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                           rp, lb, (a * kFN + b) * 1024, kSc1));
-          else
-            acc[a][b] = f32x4{nan, nan, nan, nan};
+        for (int i = 0; i < kHalfFr; ++i)
+          dma16<kSc1>(rp, region + i * 1024,
+                      (uint32_t)(lb + (h * kHalfFr + i) * 1024));
+        wait_vmcnt<0>();
+#pragma unroll
+        for (int i = 0; i < kHalfFr; ++i) {
+          const int f = h * kHalfFr + i;
+          acc[f / kFN][f % kFN] += mine[i * 64];
         }
+        if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
     }
   };
 
@@ -2401,6 +2438,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   }
   setup_d(j0);
   zero_acc();
+  tl(1);
   if constexpr (kDenseS) {
     const int nsteps = (p.k_limit + kBK - 1) / kBK;
     // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
@@ -2427,6 +2465,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
                       p_flush > 0 ? p_flush / kStepsPerBlock : -1);
     else
       pipeline(p_first, p_steps, p_flush);
+    tl(2);
     if (do_collect) collect();
   } else if constexpr (kSparseD) {
     cached_e = -1;
@@ -2434,6 +2473,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   } else {
     run_sparse(entry0, 0, entries * kStepsPerBlock);
   }
+  tl(3);
   bool empty = false;
   if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
   if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
@@ -2441,6 +2481,22 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     write_zero_tile();
   else
     write_tile(out_block);
+  if constexpr ((SPUTNIK_EXP & 512) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tl(4);
+    if (p.debug != nullptr && wave == 0 && lane < 11) {
+      // lane i < 7 writes stamp i; then the steps, the role and the row.
+      unsigned long long v = 0;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) v = lane == i ? tl_stamp[i] : v;
+      if (lane == 7) v = (unsigned long long)p_steps;
+      if (lane == 8)
+        v = (unsigned long long)(do_collect ? 2 : (p_flush > 0 ? 1 : 0));
+      if (lane == 9) v = (unsigned long long)srow;
+      if (lane == 10) v = (unsigned long long)pair_id;
+      p.debug[blockIdx.x * 16 + lane] = v;
+    }
+  }
   if constexpr ((SPUTNIK_EXP & 128) != 0) {
     if (p.debug != nullptr && lane == 0 && (wave == 0 || wave == kNW / 2)) {
       unsigned long long *o =
