@@ -23,9 +23,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
-    ap.add_argument("--ldpad", type=int, default=0,
-                    help="experiment builds: pad B's row stride by this many "
-                         "bytes (SPUTNIK_AMD_EXP_LDPAD; B reallocated)")
     ap.add_argument("--op", default="dsd", choices=["dsd", "sdd", "moe_sdd", "moe_dsd"])
     args = ap.parse_args()
     import torch
@@ -41,12 +38,6 @@ def main():
                                       np.random.default_rng(0))
         prob = bench.DsdProblem(args.m, args.k, off, idx, args.n, False,
                                 False, args.dtype, 0, dev)
-        if args.ldpad:
-            os.environ["SPUTNIK_AMD_EXP_LDPAD"] = str(args.ldpad)
-            import torch as _t
-            prob.b_vals = _t.zeros(args.k * args.n + args.k * args.ldpad // 2,
-                                   dtype=prob.b_vals.dtype, device=dev)
-            prob.B.data = prob.b_vals
         ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()
         fname = "sputnik_dsd_ex"
     elif args.op == "sdd":

@@ -49,8 +49,8 @@
 //   4: no LPT row order                  8: no XCD-aware tile map
 //  64: every DMA re-reads the first step's tiles (cache-resident: isolates
 //      the memory system from the LDS-write / issue cost of the DMA)
-// 256: flat pipeline without the steady-state LDS fragment reads
-// 1024 / 2048: flat pipeline without the S / D operand's DMA
+// 128: per-segment cycle sums of the k-loop into GemmParams::debug
+// 512: per-workgroup timeline into GemmParams::debug (scripts/exp_timeline.py)
 #ifndef SPUTNIK_EXP
 #define SPUTNIK_EXP 0
 #endif
@@ -252,81 +252,6 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
   return out;
 }
 
-// ---- ordered-stream primitives of the flat pipeline ----------------------
-// Every instruction of the flat pipeline's steady state is a volatile asm
-// statement, so hipcc keeps their program order (it never reorders volatile
-// asm) and inserts no wait for them: the pipeline counts vmcnt / lgkmcnt
-// itself and fences registers with empty "+v" statements.
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-
-// D += A * B on 16x16x32 fragments (A: src0, B: src1), f16 or bf16.
-template <typename T>
-__device__ __forceinline__ void mfma_asm(f32x4 &d, const s16x8 &a,
-                                         const s16x8 &b) {
-  if constexpr (std::is_same<T, __bf16>::value)
-    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
-                 : "+v"(d) : "v"(a), "v"(b));
-  else
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
-                 : "+v"(d) : "v"(a), "v"(b));
-}
-
-template <int kOff>
-__device__ __forceinline__ void ds_read128_asm(s16x8 &d, uint32_t addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "n"(kOff));
-}
-
-template <int kOff>
-__device__ __forceinline__ void ds_read_tr_asm(s16x4 &d, uint32_t addr) {
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"
-               : "=v"(d) : "v"(addr), "n"(kOff));
-}
-
-// Buffer descriptor words (make_buffer_rsrc(base, stride 0, kNumRecords,
-// 0x00020000)) for an "s" asm operand; every input is wave-uniform.
-__device__ __forceinline__ v4u rsrc_words(const char *base) {
-  const uint64_t a = reinterpret_cast<uint64_t>(base);
-  v4u r;
-  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xffffu);
-  r[2] = kNumRecords;
-  r[3] = 0x00020000u;
-  return r;
-}
-
-template <int N>
-constexpr int kMf_check() { return N; }
-
-// Descriptor of an empty buffer (num_records 0): every lane is out of range,
-// so an LDS-DMA from it writes zeros and moves no memory.
-__device__ __forceinline__ v4u rsrc_words_or_empty(const char *base,
-                                                   bool valid) {
-  v4u r = rsrc_words(base);
-  r[2] = ((SPUTNIK_EXP & 16384) != 0 || valid) ? kNumRecords : 0u;
-  return r;
-}
-
-// One 1 KiB LDS-DMA piece: 16 bytes per lane from r + voffset to LDS
-// [lds_addr + 16 * lane]. M0 (the LDS base) is compiler-reserved, so it is
-// saved and restored inside the statement; SALU M0 write -> LDS-DMA needs one
-// wait state.
-__device__ __forceinline__ void dma_asm(const v4u &r, uint32_t voffset,
-                                        uint32_t lds_addr) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voffset), "s"(r), "s"(lds_addr)
-      : "memory");
-}
-
 // Maps the launch index to a tile index so that each XCD (blocks b and b+8
 // share one) walks a contiguous run of tiles. Bijective for any grid size.
 __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
@@ -343,7 +268,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
 // sets the register budget through __launch_bounds__ and must match the LDS
 // footprint).
 template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_,
-          int STAGGER_ = 0, int KSPLIT_ = 1, int FLAT_ = 0>
+          int STAGGER_ = 0, int KSPLIT_ = 1>
 struct TileConfig {
   static constexpr int kBN = BN_, kWM = WM_, kWN = WN_, kBK = BK_;
   static constexpr int kStages = STAGES_, kWGs = WGS_;
@@ -356,13 +281,6 @@ struct TileConfig {
   // SIMD) run one barrier apart, so one half's DMA/read phase overlaps the
   // other half's MFMA phase (needs kStages >= 4; see the pipeline).
   static constexpr bool kStagger = STAGGER_ != 0;
-  // kFlat: every wave runs the same step, one barrier per step; its MFMAs,
-  // the LDS reads of the next step and the DMA of the next block are
-  // interleaved in one ordered instruction stream (pipeline_flat), so the
-  // two waves of a SIMD cover each other's memory issue with MFMAs instead
-  // of alternating whole phases.
-  static constexpr bool kFlat = FLAT_ != 0;
-  static constexpr bool kSplit = FLAT_ == 2;
 };
 
 // 8 waves, 64x64 each, BK=64, one workgroup per CU (first-generation DSD/DDS).
@@ -384,12 +302,6 @@ using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 // (the whole 160 KiB LDS; the sparse index list is then read with scalar
 // loads, not staged), pair-balanced across block-rows (dispatch.cpp).
 using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
-// The same tile and ring on the flat interleaved pipeline.
-using CfgWide8F = TileConfig<512, 2, 4, 32, 4, 1, 0, 1, 1>;
-// Flat pipeline with split DMA roles (pipeline_split): waves 0-3 stream the
-// dense operand two steps ahead, waves 4-7 the sparse blocks about six steps
-// ahead (their reads go beyond L2), each with its own vmcnt.
-using CfgWide8P = TileConfig<512, 2, 4, 32, 4, 1, 0, 1, 2>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 // SDD, one block per workgroup with K split inside it: 8 waves in two
@@ -483,10 +395,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // Index list staged per chunk in LDS (smaller when three workgroups share
   // a CU); staggered configs read it with scalar loads instead.
   constexpr bool kScalarIdx =
-      (Cfg::kStagger || Cfg::kFlat) && !kSparseIn && !kSparseD;
-  static_assert(!Cfg::kFlat || (kStages == 4 && kBlock / kBK == 4 &&
-                                !kSparseOut && !Cfg::kStagger),
-                "flat pipeline: DSD / DDS, 4 slots of one quarter block");
+      Cfg::kStagger && !kSparseIn && !kSparseD;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
   constexpr bool kDenseS = kSparseOut && !kSparseIn;  // SDD
   static_assert(!kSparseIn || (kSparseOut &&
@@ -1222,721 +1131,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     if (!lag) __builtin_amdgcn_s_barrier();
   };
 
-  // ---- DSD / DDS on the flat configs (Cfg::kFlat). One barrier per
-  // 32-deep step; slot h of the 4-slot ring always holds quarter h of a
-  // stored block. Step h of block b, after its barrier, is ONE ordered
-  // instruction stream: the 32 MFMAs of (b, h) on registers read in the
-  // previous step, interleaved with the LDS reads of the next step's
-  // fragments and the LDS-DMA of quarter h of block b + 1 into slot h.
-  //  - RAW: a wave reads slot s after the barrier that follows every wave's
-  //    counted vmcnt wait for its own pieces of s.
-  //  - WAR: slot h was last read during step (b, h - 1) (drained with
-  //    lgkmcnt(0) before this step's barrier), so DMA(b + 1, h) may refill
-  //    it once the barrier is passed.
-  //  - vmcnt: before step (b, h) a wave needs its DMA of the slot it reads
-  //    next; two quarters issued after that one stay in flight (vmcnt(2
-  //    groups)), i.e. the DMA has three steps to land.
-  // The MFMA operands stay in registers between steps (cur / nxt swap by
-  // unrolling), so the compiler inserts nothing into the stream.
-  struct FFrags {
-    s16x8 a[kFM];               // S operand (k-contiguous image)
-    s16x4 alo[kFM], ahi[kFM];   // S operand (m-contiguous image)
-    s16x8 b[kFN];
-    s16x4 blo[kFN], bhi[kFN];
-  };
-  auto pipeline_flat = [&](int e0, int nblk, int flush_blk) {
-   if constexpr (Cfg::kFlat && !Cfg::kSplit) {
-    if (nblk <= 0) return;
-    auto entry = [&](int x) {
-      return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
-    };
-    int nk = 0, nbk = 0;  // (k-block, storage block) of the next block
-    auto load_idx = [&](int e) {
-      const int ge = entry(e);
-      nk = scalar_load_short(p.s_indices, ge);
-      nbk = p.s_block_offsets != nullptr ? scalar_load_int(p.s_block_offsets, ge)
-                                         : ge;
-    };
-    const char *cs = nullptr, *cd = nullptr;  // bases of the block being fed
-    auto take_next = [&]() {
-      asm volatile("" : "+s"(nk), "+s"(nbk));  // after the previous stream
-      cs = p.s_data + (long long)nbk * (kBlock * kBlock * 2);
-      const long long kg = (long long)nk * kBlock;
-      cd = kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
-                : p.d_data + kg * p.d_ld + (long long)j0 * 2;
-    };
-    // LDS byte address of the ring and this wave's DMA destinations.
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(
-        (__attribute__((address_space(3))) char *)(lds));
-    const uint32_t dst_s = __builtin_amdgcn_readfirstlane(
-        lds0 + (uint32_t)(wave * kSInstr * 1024));
-    const uint32_t dst_d = __builtin_amdgcn_readfirstlane(
-        lds0 + (uint32_t)(kSBytes + wave * kDInstr * 1024));
-    // Piece q of quarter h (q < kSInstr: S, else D) from the current bases.
-    auto dma_piece = [&](auto h_c, auto q_c, const v4u &rs, const v4u &rd) {
-      constexpr int H = decltype(h_c)::value;
-      constexpr int Q = decltype(q_c)::value;
-      if constexpr ((SPUTNIK_EXP & 2) != 0) return;
-      if constexpr ((SPUTNIK_EXP & 1024) != 0 && Q < kSInstr) return;
-      if constexpr ((SPUTNIK_EXP & 2048) != 0 && Q >= kSInstr) return;
-      if constexpr (Q < kSInstr)
-        dma_asm(rs, s_off[Q], dst_s + H * kStageBytes + Q * 1024);
-      else
-        dma_asm(rd, d_off[Q - kSInstr],
-                dst_d + H * kStageBytes + (Q - kSInstr) * 1024);
-    };
-    auto quarter_rsrc = [&](auto h_c, v4u &rs, v4u &rd) {
-      constexpr int H = decltype(h_c)::value;
-      rs = rsrc_words(cs + (kSKC ? H * (kBK * 2) : H * (kBK * 256)));
-      rd = rsrc_words(cd + (kDKC ? (long long)H * (kBK * 2)
-                                 : (long long)H * kBK * p.d_ld));
-    };
-    auto dma_quarter = [&](auto h_c) {
-      v4u rs, rd;
-      quarter_rsrc(h_c, rs, rd);
-      static_for<0, kGroup>([&](auto q_c) { dma_piece(h_c, q_c, rs, rd); });
-    };
-
-    // Per-lane LDS read offsets inside a slot, fragment f (as read_kc /
-    // read_mn). A k-contiguous operand's fragments sit 16 rows (1 KiB) apart
-    // at one base; an m/n-contiguous one needs a base per fragment (XOR).
-    constexpr int kSImgRow = kSKC ? kKcRow : kBM * 2;
-    constexpr int kDImgRow = kDKC ? kKcRow : kDRowBytes;
-    auto kc_off = [&](int row0) -> uint32_t {
-      const int row = row0 + (lane & 15);
-      const int c = lane >> 4;
-      return (uint32_t)(row * kKcRow + ((c ^ kc_key<kBK / 8>(row)) << 4));
-    };
-    auto mn_off = [&](int col0, int row_bytes) -> uint32_t {
-      const int q = (lane >> 2) & 3, pp = lane & 3, g = lane >> 4;
-      const int k = 8 * g + q;
-      return (uint32_t)(k * row_bytes + (pp << 3) +
-                        (((col0 >> 4) ^ tr_key(k)) << 5));
-    };
-    // An m/n-contiguous operand's fragment f (16 columns further) differs
-    // only in the XOR-swizzled sector: mn_off(c0 + 16 f) = mn_off(c0) ^
-    // (f << 5) when c0 / 16 has clear low bits (c0 = 64 wm or 128 wn), and a
-    // slot base has clear bits 5-7, so one per-lane offset serves them all.
-    const uint32_t a_l = kSKC ? kc_off(row_w) : mn_off(row_w, kSImgRow);
-    const uint32_t b_l = kDKC ? kc_off(col_w) : mn_off(col_w, kDImgRow);
-    static_assert((kStageBytes & 0xff) == 0 && (kSBytes & 0xff) == 0 &&
-                      kFM <= 4 && kFN <= 8,
-                  "XOR addressing of the fragments");
-    // Read pieces of one step: S fragments first, then D; a k-contiguous
-    // fragment is one ds_read_b128, an m/n-contiguous one two transpose reads.
-    constexpr int kAP = kSKC ? kFM : 2 * kFM;
-    constexpr int kBP = kDKC ? kFN : 2 * kFN;
-    constexpr int kRP = kAP + kBP;
-    auto read_piece = [&](auto slot_c, auto r_c, FFrags &F,
-                          const uint32_t *abase, const uint32_t *bbase) {
-      constexpr int SL = decltype(slot_c)::value;
-      constexpr int R = decltype(r_c)::value;
-      (void)SL;
-      if constexpr ((SPUTNIK_EXP & 256) != 0) return;
-      if constexpr (R < kAP) {
-        if constexpr (kSKC) {
-          ds_read128_asm<R * 16 * kKcRow>(F.a[R], abase[0]);
-        } else {
-          constexpr int f = R / 2;
-          if constexpr (R % 2 == 0)
-            ds_read_tr_asm<0>(F.alo[f], abase[f]);
-          else
-            ds_read_tr_asm<4 * kSImgRow>(F.ahi[f], abase[f]);
-        }
-      } else {
-        constexpr int Rb = R - kAP;
-        if constexpr (kDKC) {
-          ds_read128_asm<Rb * 16 * kKcRow>(F.b[Rb], bbase[0]);
-        } else {
-          constexpr int f = Rb / 2;
-          if constexpr (Rb % 2 == 0)
-            ds_read_tr_asm<0>(F.blo[f], bbase[f]);
-          else
-            ds_read_tr_asm<4 * kDImgRow>(F.bhi[f], bbase[f]);
-        }
-      }
-    };
-    auto slot_bases = [&](int slot, uint32_t *abase, uint32_t *bbase) {
-      // Opaque slot offset: a compile-time one lets hipcc precompute every
-      // slot's addresses outside the loop (4x the address registers).
-      uint32_t sb = lds0 + (uint32_t)(slot * kStageBytes);
-      asm volatile("" : "+s"(sb));
-      const uint32_t a0 = sb + a_l, b0 = sb + kSBytes + b_l;
-#pragma unroll
-      for (int f = 0; f < (kSKC ? 1 : kFM); ++f) abase[f] = a0 ^ (f << 5);
-#pragma unroll
-      for (int f = 0; f < (kDKC ? 1 : kFN); ++f) bbase[f] = b0 ^ (f << 5);
-    };
-    // Registers of a step's fragments are final only after its lgkmcnt(0):
-    // fence them so no copy or use is scheduled above the wait.
-    auto fence_frags = [&](FFrags &F) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) {
-        if constexpr (kSKC) {
-          asm volatile("" : "+v"(F.a[f]));
-        } else {
-          asm volatile("" : "+v"(F.alo[f]), "+v"(F.ahi[f]));
-        }
-      }
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) {
-        if constexpr (kDKC) {
-          asm volatile("" : "+v"(F.b[f]));
-        } else {
-          asm volatile("" : "+v"(F.blo[f]), "+v"(F.bhi[f]));
-        }
-      }
-    };
-    auto fence_acc = [&]() {
-#pragma unroll
-      for (int a = 0; a < kFM; ++a)
-#pragma unroll
-        for (int b = 0; b < kFN; ++b) asm volatile("" : "+v"(acc[a][b]));
-    };
-    auto opnd_a = [&](FFrags &F, int f) -> s16x8 {
-      if constexpr (kSKC) return F.a[f];
-      else return __builtin_shufflevector(F.alo[f], F.ahi[f], 0, 1, 2, 3, 4, 5, 6, 7);
-    };
-    auto opnd_b = [&](FFrags &F, int f) -> s16x8 {
-      if constexpr (kDKC) return F.b[f];
-      else return __builtin_shufflevector(F.blo[f], F.bhi[f], 0, 1, 2, 3, 4, 5, 6, 7);
-    };
-    constexpr int kMf = kFM * kFN;  // MFMAs per step
-    // Stream schedule: DMA piece q after MFMA dma_pos(q), read piece r after
-    // MFMA read_pos(r) (spread over the step; the first reads early, so the
-    // next step's fragments land under this step's MFMAs).
-    struct Sched {
-      static constexpr int dma_pos(int q) { return 2 + q * (kMf - 4) / kGroup; }
-      static constexpr int read_pos(int r) { return 1 + r * (kMf - 3) / kRP; }
-      static constexpr int dma_at(int m) {
-        for (int q = 0; q < kGroup; ++q)
-          if (dma_pos(q) == m) return q;
-        return -1;
-      }
-      static constexpr int reads_from(int m) {  // first piece at or after m
-        for (int r = 0; r < kRP; ++r)
-          if (read_pos(r) >= m) return r;
-        return kRP;
-      }
-    };
-    static_assert(Sched::dma_pos(kGroup - 1) < kMf &&
-                      Sched::read_pos(kRP - 1) < kMf,
-                  "flat schedule");
-    auto fstep = [&](auto h_c, auto last_c, FFrags &cur, FFrags &nxt) {
-      constexpr int H = decltype(h_c)::value;
-      constexpr bool LAST = decltype(last_c)::value;
-      constexpr bool kNext = !(LAST && H == 3);
-      constexpr bool kDma = !LAST;
-      constexpr int kRS = (H + 1) & 3;  // slot whose fragments are read
-      if constexpr (kNext) {
-        wait_vmcnt<(LAST ? 2 - H : 2) * kGroup>();
-        __builtin_amdgcn_s_barrier();
-      }
-      v4u rs, rd;
-      if constexpr (kDma) quarter_rsrc(h_c, rs, rd);
-      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
-      if constexpr (kNext) slot_bases(kRS, abase, bbase);
-      s16x8 ca[kFM], cb[kFN];
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) ca[f] = opnd_a(cur, f);
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) cb[f] = opnd_b(cur, f);
-      static_for<0, kMf>([&](auto m_c) {
-        constexpr int m = decltype(m_c)::value;
-        constexpr int fa = m % kFM, fb = m / kFM;
-        if constexpr ((SPUTNIK_EXP & 1) == 0) {
-          if constexpr (kOutT)
-            mfma_asm<T>(acc[fa][fb], ca[fa], cb[fb]);
-          else
-            mfma_asm<T>(acc[fa][fb], cb[fb], ca[fa]);
-        }
-        constexpr int q = Sched::dma_at(m);
-        if constexpr (kDma && q >= 0)
-          dma_piece(h_c, std::integral_constant<int, q>{}, rs, rd);
-        constexpr int r0 = Sched::reads_from(m), r1 = Sched::reads_from(m + 1);
-        if constexpr (kNext && r1 > r0) {
-          static_for<r0, r1>([&](auto r_c) {
-            read_piece(std::integral_constant<int, kRS>{}, r_c, nxt, abase,
-                       bbase);
-          });
-        }
-      });
-      // The current operands stay allocated until the step's end: no read
-      // of the next step may land in a register an MFMA of this step reads.
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) asm volatile("" :: "v"(ca[f]));
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) asm volatile("" :: "v"(cb[f]));
-      if constexpr (kNext) fence_frags(nxt);
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    // Accumulators written by VALU (zeroing) before an MFMA reads them, or
-    // by an MFMA before VALU / VMEM reads them: hipcc pads neither across
-    // asm, so pad here (16 wait states covers both directions).
-    auto pad_acc = [&]() {
-      fence_acc();
-      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-      fence_acc();
-    };
-
-    // Prologue: block 0 into slots 0..3 (slot 3 after a barrier: the
-    // barrier-free row ranking keeps per-wave scratch there), its quarter 0
-    // read into f0, block 1's bases ready.
-    FFrags f0, f1;
-    load_idx(e0);
-    take_next();
-    dma_quarter(I0{});
-    dma_quarter(I1{});
-    dma_quarter(I2{});
-    __builtin_amdgcn_s_barrier();
-    dma_quarter(I3{});
-    load_idx(e0 + min(1, nblk - 1));
-    wait_vmcnt<3 * kGroup>();
-    __builtin_amdgcn_s_barrier();
-    {
-      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
-      slot_bases(0, abase, bbase);
-      static_for<0, kRP>([&](auto r_c) {
-        read_piece(I0{}, r_c, f0, abase, bbase);
-      });
-      fence_frags(f0);
-    }
-    take_next();
-    load_idx(e0 + min(2, nblk - 1));
-    pad_acc();
-    int b = 0;
-    for (; b + 1 < nblk; ++b) {
-      fstep(I0{}, std::false_type{}, f0, f1);
-      fstep(I1{}, std::false_type{}, f1, f0);
-      fstep(I2{}, std::false_type{}, f0, f1);
-      fstep(I3{}, std::false_type{}, f1, f0);
-      if constexpr (kPairs) {
-        if (b + 1 == flush_blk) {
-          pad_acc();
-          publish();
-          pad_acc();
-        }
-      }
-      take_next();  // block b + 2 (clamped)
-      load_idx(e0 + min(b + 3, nblk - 1));
-    }
-    fstep(I0{}, std::true_type{}, f0, f1);
-    fstep(I1{}, std::true_type{}, f1, f0);
-    fstep(I2{}, std::true_type{}, f0, f1);
-    fstep(I3{}, std::true_type{}, f1, f0);
-    pad_acc();
-    if constexpr (kPairs) {
-      if (b + 1 == flush_blk) {
-        publish();
-        pad_acc();
-      }
-    }
-   }
-  };
-
-  // ---- DSD / DDS, flat pipeline with split DMA roles (Cfg::kSplit) -------
-  // The sparse blocks S come from beyond L2 (every XCD reads all of them
-  // once), the dense panel D mostly from L2, and a wave's vmcnt retires its
-  // DMA in issue order, so one wave cannot keep S far ahead while waiting on
-  // D. Waves 0-3 (one per SIMD) therefore issue only D, two steps ahead, into
-  // a 3-slot ring; waves 4-7 only S, in full 128-byte lines, 5-6 steps ahead,
-  // into a 4-slot ring of two-step images; every wave computes its 64 x 128
-  // sub-tile from both rings. LDS: [S ring 4 x 16 KiB][D ring 3 x 32 KiB].
-  // Steps past the row's end issue out-of-range DMA (zeros, no memory
-  // traffic) so every wait count is a constant.
-  //  - D: step j issues D(j + 3) into slot j % 3 (held D(j), read in step
-  //    j - 1); before step j a D-wave needs D(j + 1): vmcnt(8).
-  //  - S: step j issues half (j + 1) & 1 of image v = (j + 1) / 2 + 3 into
-  //    slot v % 4 (held v - 4, last read in step 2v - 8 < j); before step j
-  //    an S-wave needs image (j + 1) / 2: vmcnt(10) for even j, 8 for odd.
-  auto pipeline_split = [&](int e0, int nblk, int flush_blk) {
-   if constexpr (Cfg::kSplit) {
-    if (nblk <= 0) return;
-    constexpr int kSImg = 2 * kSBytes;       // S image: two steps, 16 KiB
-    constexpr int kSRing = 4 * kSImg;
-    constexpr int kDPieces = kDBytes / 1024 / (kNW / 2);  // per D-wave
-    constexpr int kSPieces = kSImg / 1024 / (kNW / 2);    // per S-wave, image
-    constexpr int kSImgRow = kSKC ? 128 : kBM * 2;         // S image row bytes
-    static_assert(kSRing + 3 * kDBytes <= kRingBytes && kDPieces == 8 &&
-                      kSPieces == 4 && kMf_check<kFM * kFN>() == 32,
-                  "split pipeline geometry");
-    const bool dwave = wave < kNW / 2;
-    const int rw = dwave ? wave : wave - kNW / 2;  // index inside the role
-    auto entry = [&](int x) {
-      return x < idx_split ? idx_base + x : idx_base2 + (x - idx_split);
-    };
-    // (k-block, storage block) of blocks b .. b + 3 (b + 3 prefetched).
-    int k0 = 0, k1 = 0, k2 = 0, k3 = 0, s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    auto load_e = [&](int x, int &kk, int &ss) {
-      const int ge = entry(e0 + min(x, nblk - 1));
-      kk = scalar_load_short(p.s_indices, ge);
-      ss = p.s_block_offsets != nullptr ? scalar_load_int(p.s_block_offsets, ge)
-                                        : ge;
-    };
-    // Per-lane DMA offsets: D-waves 8 pieces of a D image, S-waves 4 of an
-    // S image (2 per step).
-    uint32_t voff[kDPieces];
-#pragma unroll
-    for (int q = 0; q < kDPieces; ++q) {
-      uint32_t off = 0;
-      if (dwave) {
-        const int g = rw * kDPieces + q;
-        bool ok;
-        if constexpr (kDKC) {
-          const int jj = kKcRowsPerInstr * g + lane / kKcChunks;
-          const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(jj);
-          off = (uint32_t)(jj * p.d_ld + c * 16);
-          ok = j0 + jj < p.j_limit;
-        } else {
-          const int k = kDRowsPerInstr * g + lane / kDChunksPerRow;
-          const int pc = lane % kDChunksPerRow;
-          const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
-          off = (uint32_t)(k * p.d_ld + c * 16);
-          ok = j0 + c * 8 < p.j_limit;
-        }
-        if (!ok) off = kOOB;
-      } else if (q < kSPieces) {
-        const int g = rw * kSPieces + q;
-        if constexpr (kSKC) {  // [128 rows][64 k]: 8 rows of 128 B a piece
-          const int row = 8 * g + lane / 8;
-          const int c = (lane % 8) ^ kc_key<8>(row);
-          off = (uint32_t)(row * 256 + c * 16);
-        } else {  // [64 k][128 m]: 4 rows of 256 B a piece
-          const int k = 4 * g + lane / 16;
-          const int pc = lane % 16;
-          const int c = (((pc >> 1) ^ tr_key(k)) << 1) | (pc & 1);
-          off = (uint32_t)(k * 256 + c * 16);
-        }
-      }
-      voff[q] = off;
-    }
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(
-        (__attribute__((address_space(3))) char *)(lds));
-    const uint32_t lds_s = lds0, lds_d = lds0 + kSRing;
-    // Base of D image (block with k-block kb, quarter q); of S image (block
-    // with storage block sb, k-half dq).
-    auto d_src = [&](int kb, int q) -> const char * {
-      const long long kg = (long long)kb * kBlock + q * kBK;
-      return kDKC ? p.d_data + (long long)j0 * p.d_ld + kg * 2
-                  : p.d_data + kg * p.d_ld + (long long)j0 * 2;
-    };
-    auto s_src = [&](int sb, int dq) -> const char * {
-      return p.s_data + (long long)sb * (kBlock * kBlock * 2) +
-             (kSKC ? dq * 128 : dq * (64 * 256));
-    };
-    // Read offsets (as pipeline_flat; the S image rows are 128 B when
-    // k-contiguous, with 8 chunks, and kk selects the step's k-half).
-    auto kc_off_s = [&](int kk) -> uint32_t {
-      const int row = row_w + (lane & 15);
-      const int c = 4 * kk + (lane >> 4);
-      return (uint32_t)(row * 128 + ((c ^ kc_key<8>(row)) << 4));
-    };
-    auto mn_off = [&](int col0, int row_bytes, int kk) -> uint32_t {
-      const int q = (lane >> 2) & 3, pp = lane & 3, g = lane >> 4;
-      const int k = 32 * kk + 8 * g + q;
-      return (uint32_t)(k * row_bytes + (pp << 3) +
-                        (((col0 >> 4) ^ tr_key(k)) << 5));
-    };
-    auto kc_off_d = [&](int row0) -> uint32_t {
-      const int row = row0 + (lane & 15);
-      const int c = lane >> 4;
-      return (uint32_t)(row * kKcRow + ((c ^ kc_key<kBK / 8>(row)) << 4));
-    };
-    const uint32_t a_l0 = kSKC ? kc_off_s(0) : mn_off(row_w, kSImgRow, 0);
-    const uint32_t a_l1 = kSKC ? kc_off_s(1) : mn_off(row_w, kSImgRow, 1);
-    const uint32_t b_l = kDKC ? kc_off_d(col_w) : mn_off(col_w, kDRowBytes, 0);
-    constexpr int kDImgRow = kDKC ? kKcRow : kDRowBytes;
-    constexpr int kAP = kSKC ? kFM : 2 * kFM;
-    constexpr int kBP = kDKC ? kFN : 2 * kFN;
-    constexpr int kRP = kAP + kBP;
-    constexpr int kMf = kFM * kFN;
-    auto read_piece = [&](auto r_c, FFrags &F, const uint32_t *abase,
-                          const uint32_t *bbase) {
-      constexpr int R = decltype(r_c)::value;
-      if constexpr ((SPUTNIK_EXP & 256) != 0) return;
-      if constexpr (R < kAP) {
-        if constexpr (kSKC) {
-          ds_read128_asm<R * 16 * 128>(F.a[R], abase[0]);
-        } else {
-          constexpr int f = R / 2;
-          if constexpr (R % 2 == 0)
-            ds_read_tr_asm<0>(F.alo[f], abase[f]);
-          else
-            ds_read_tr_asm<4 * kSImgRow>(F.ahi[f], abase[f]);
-        }
-      } else {
-        constexpr int Rb = R - kAP;
-        if constexpr (kDKC) {
-          ds_read128_asm<Rb * 16 * kKcRow>(F.b[Rb], bbase[0]);
-        } else {
-          constexpr int f = Rb / 2;
-          if constexpr (Rb % 2 == 0)
-            ds_read_tr_asm<0>(F.blo[f], bbase[f]);
-          else
-            ds_read_tr_asm<4 * kDImgRow>(F.bhi[f], bbase[f]);
-        }
-      }
-    };
-    // Fragment bases of one step: S image slot / k-half, D slot (opaque, so
-    // no slot's addresses are hoisted out of the loop).
-    auto step_bases = [&](uint32_t s_img, int kk, uint32_t d_img,
-                          uint32_t *abase, uint32_t *bbase) {
-      asm volatile("" : "+s"(s_img), "+s"(d_img));
-      const uint32_t a0 = s_img + (kk ? a_l1 : a_l0), b0 = d_img + b_l;
-#pragma unroll
-      for (int f = 0; f < (kSKC ? 1 : kFM); ++f) abase[f] = a0 ^ (f << 5);
-#pragma unroll
-      for (int f = 0; f < (kDKC ? 1 : kFN); ++f) bbase[f] = b0 ^ (f << 5);
-    };
-    auto fence_frags = [&](FFrags &F) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) {
-        if constexpr (kSKC) asm volatile("" : "+v"(F.a[f]));
-        else asm volatile("" : "+v"(F.alo[f]), "+v"(F.ahi[f]));
-      }
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) {
-        if constexpr (kDKC) asm volatile("" : "+v"(F.b[f]));
-        else asm volatile("" : "+v"(F.blo[f]), "+v"(F.bhi[f]));
-      }
-    };
-    auto fence_acc = [&]() {
-#pragma unroll
-      for (int a = 0; a < kFM; ++a)
-#pragma unroll
-        for (int b = 0; b < kFN; ++b) asm volatile("" : "+v"(acc[a][b]));
-    };
-    auto pad_acc = [&]() {
-      fence_acc();
-      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-      fence_acc();
-    };
-    auto opnd_a = [&](FFrags &F, int f) -> s16x8 {
-      if constexpr (kSKC) return F.a[f];
-      else return __builtin_shufflevector(F.alo[f], F.ahi[f], 0, 1, 2, 3, 4, 5, 6, 7);
-    };
-    auto opnd_b = [&](FFrags &F, int f) -> s16x8 {
-      if constexpr (kDKC) return F.b[f];
-      else return __builtin_shufflevector(F.blo[f], F.bhi[f], 0, 1, 2, 3, 4, 5, 6, 7);
-    };
-    // One role's DMA of a step: the D-waves' 8 pieces or the S-waves' 2
-    // (pieces 2..7 are skipped by a uniform branch).
-    struct Dma { v4u r; uint32_t m0; };
-    auto dma_k = [&](const Dma &d, int k, uint32_t vo) {
-      if constexpr ((SPUTNIK_EXP & 2) != 0) return;
-      if constexpr ((SPUTNIK_EXP & 1024) != 0) { if (!dwave) return; }
-      if constexpr ((SPUTNIK_EXP & 2048) != 0) { if (dwave) return; }
-      dma_asm(d.r, vo, d.m0 + k * 1024);
-    };
-    struct Sched {
-      static constexpr int dma_pos(int k) { return 1 + 4 * k; }  // k < 8
-      static constexpr int read_pos(int r) { return 2 + r * (kMf - 4) / kRP; }
-      static constexpr int dma_at(int m) {
-        for (int k = 0; k < 8; ++k)
-          if (dma_pos(k) == m) return k;
-        return -1;
-      }
-      static constexpr int reads_from(int m) {
-        for (int r = 0; r < kRP; ++r)
-          if (read_pos(r) >= m) return r;
-        return kRP;
-      }
-    };
-    int b = 0;      // current block
-    int dsl = 0;    // D slot of step j (j % 3)
-    // Step H of block b (j = 4b + H).
-    auto sstep = [&](auto h_c, auto last_c, FFrags &cur, FFrags &nxt) {
-      constexpr int H = decltype(h_c)::value;
-      constexpr bool LAST = decltype(last_c)::value;
-      constexpr bool kNext = !(LAST && H == 3);
-      if constexpr (kNext) {
-        if constexpr ((SPUTNIK_EXP & 8192) != 0)
-          wait_vmcnt<0>();
-        else if (dwave) {
-          if constexpr ((SPUTNIK_EXP & 32768) != 0) wait_vmcnt<0>();
-          else wait_vmcnt<8>();
-        } else if constexpr ((SPUTNIK_EXP & 65536) != 0)
-          wait_vmcnt<0>();
-        else if constexpr (H % 2 == 0)
-          wait_vmcnt<10>();
-        else
-          wait_vmcnt<8>();
-        __builtin_amdgcn_s_barrier();
-        if constexpr ((SPUTNIK_EXP & 131072) != 0) {
-          if (!dwave) __builtin_amdgcn_s_sleep(30);
-        }
-        if constexpr ((SPUTNIK_EXP & 262144) != 0) {
-          if (dwave) __builtin_amdgcn_s_sleep(30);
-        }
-      }
-      // This step's DMA (role-selected SGPRs).
-      Dma d;
-      {
-        // D(j + 3): block b, quarter 3 (H = 0) or block b + 1, quarter H - 1.
-        const int dkb = H == 0 ? k0 : k1;
-        const bool dval = H == 0 ? true : b + 1 < nblk;
-        // S: image v = 2b + 3 (H = 0), 2b + 4 (H = 1, 2), 2b + 5 (H = 3);
-        // block v / 2, k-half v % 2, piece half (H + 1) & 1.
-        constexpr int kVoff = H == 0 ? 3 : (H == 3 ? 5 : 4);
-        const int v = 2 * b + kVoff;
-        const int sblk = H == 0 ? s1 : s2;
-        const bool sval = v / 2 < nblk;
-        constexpr int kHalf = (H + 1) & 1;
-        const uint32_t dm0 = lds_d + (uint32_t)(dsl * kDBytes) +
-                             (uint32_t)(rw * kDPieces * 1024);
-        const uint32_t sm0 = lds_s + (uint32_t)((v & 3) * kSImg) +
-                             (uint32_t)((rw * kSPieces + 2 * kHalf) * 1024);
-        const v4u rdv = rsrc_words_or_empty(d_src(dkb, (H + 3) & 3), dval);
-        const v4u rsv = rsrc_words_or_empty(s_src(sblk, kVoff & 1), sval);
-        d.r = dwave ? rdv : rsv;
-        d.m0 = __builtin_amdgcn_readfirstlane(dwave ? dm0 : sm0);
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-          d.r[w] = __builtin_amdgcn_readfirstlane(d.r[w]);
-      }
-      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
-      if constexpr (kNext) {
-        // Step j + 1: S image (j + 1) / 2 = 2b + (H + 1) / 2, k-half
-        // (H + 1) & 1; D slot (j + 1) % 3.
-        const int simg = (2 * b + (H + 1) / 2) & 3;
-        const int dnext = dsl == 2 ? 0 : dsl + 1;
-        step_bases(lds_s + (uint32_t)(simg * kSImg), (H + 1) & 1,
-                   lds_d + (uint32_t)(dnext * kDBytes), abase, bbase);
-      }
-      s16x8 ca[kFM], cb[kFN];
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) ca[f] = opnd_a(cur, f);
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) cb[f] = opnd_b(cur, f);
-      static_for<0, kMf>([&](auto m_c) {
-        constexpr int m = decltype(m_c)::value;
-        constexpr int fa = m % kFM, fb = m / kFM;
-        if constexpr ((SPUTNIK_EXP & 1) == 0) {
-          if constexpr (kOutT)
-            mfma_asm<T>(acc[fa][fb], ca[fa], cb[fb]);
-          else
-            mfma_asm<T>(acc[fa][fb], cb[fb], ca[fa]);
-        }
-        // The last step has no barrier, so it issues no DMA: its slots may
-        // still be read by other waves.
-        constexpr int k = kNext ? Sched::dma_at(m) : -1;
-        if constexpr (k >= 0) {
-          if constexpr (k < 2) {
-            // S-waves take the pieces of this step's image half.
-            constexpr int kHalf = (H + 1) & 1;
-            dma_k(d, k, kHalf == 0 ? voff[k]
-                                   : (dwave ? voff[k] : voff[k + 2]));
-          } else {
-            if (dwave) dma_k(d, k, voff[k]);
-          }
-        }
-        constexpr int r0 = Sched::reads_from(m), r1 = Sched::reads_from(m + 1);
-        if constexpr (kNext && r1 > r0) {
-          static_for<r0, r1>([&](auto r_c) { read_piece(r_c, nxt, abase, bbase); });
-        }
-      });
-#pragma unroll
-      for (int f = 0; f < kFM; ++f) asm volatile("" :: "v"(ca[f]));
-#pragma unroll
-      for (int f = 0; f < kFN; ++f) asm volatile("" :: "v"(cb[f]));
-      if constexpr (kNext) fence_frags(nxt);
-      dsl = dsl == 2 ? 0 : dsl + 1;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-
-    // Prologue (after a barrier: the row ranking's per-wave scratch lies in
-    // the ring): D(0..2) and S images 0..2 plus half 0 of image 3, then the
-    // fragments of step 0.
-    FFrags f0, f1;
-    load_e(0, k0, s0);
-    load_e(1, k1, s1);
-    load_e(2, k2, s2);
-    asm volatile("" : "+s"(k0), "+s"(s0), "+s"(k1), "+s"(s1), "+s"(k2),
-                 "+s"(s2));
-    __builtin_amdgcn_s_barrier();
-    {
-      if (dwave) {
-        static_for<0, 3>([&](auto q_c) {
-          constexpr int Q = decltype(q_c)::value;
-          Dma d;
-          d.r = rsrc_words(d_src(k0, Q));
-          d.m0 = __builtin_amdgcn_readfirstlane(
-              lds_d + (uint32_t)(Q * kDBytes + rw * kDPieces * 1024));
-          static_for<0, kDPieces>([&](auto k_c) {
-            constexpr int K = decltype(k_c)::value;
-            dma_k(d, K, voff[K]);
-          });
-        });
-      } else {
-        // Images 0 (block 0, half 0), 1 (block 0, half 1), 2 (block 1, half
-        // 0), and half 0 of image 3 (block 1, half 1).
-        static_for<0, 4>([&](auto v_c) {
-          constexpr int V = decltype(v_c)::value;
-          Dma d;
-          d.r = rsrc_words_or_empty(s_src(V < 2 ? s0 : s1, V & 1),
-                                    V / 2 < nblk);
-          d.m0 = __builtin_amdgcn_readfirstlane(
-              lds_s + (uint32_t)(V * kSImg + rw * kSPieces * 1024));
-          static_for<0, (V < 3 ? kSPieces : 2)>([&](auto k_c) {
-            constexpr int K = decltype(k_c)::value;
-            dma_k(d, K, voff[K]);
-          });
-        });
-      }
-    }
-    load_e(3, k3, s3);
-    if (dwave) wait_vmcnt<16>(); else wait_vmcnt<10>();
-    __builtin_amdgcn_s_barrier();
-    {
-      uint32_t abase[kSKC ? 1 : kFM], bbase[kDKC ? 1 : kFN];
-      step_bases(lds_s, 0, lds_d, abase, bbase);
-      static_for<0, kRP>([&](auto r_c) { read_piece(r_c, f0, abase, bbase); });
-      fence_frags(f0);
-    }
-    pad_acc();
-    auto rotate = [&]() {  // block b + 1 begins: entries move down one
-      asm volatile("" : "+s"(k3), "+s"(s3));
-      k0 = k1; s0 = s1; k1 = k2; s1 = s2; k2 = k3; s2 = s3;
-      load_e(b + 4, k3, s3);  // b is the finished block
-    };
-    for (; b + 1 < nblk; ++b) {
-      sstep(I0{}, std::false_type{}, f0, f1);
-      sstep(I1{}, std::false_type{}, f1, f0);
-      sstep(I2{}, std::false_type{}, f0, f1);
-      sstep(I3{}, std::false_type{}, f1, f0);
-      if constexpr (kPairs) {
-        if (b + 1 == flush_blk) {
-          pad_acc();
-          publish();
-          pad_acc();
-        }
-      }
-      rotate();
-    }
-    sstep(I0{}, std::true_type{}, f0, f1);
-    sstep(I1{}, std::true_type{}, f1, f0);
-    sstep(I2{}, std::true_type{}, f0, f1);
-    sstep(I3{}, std::true_type{}, f1, f0);
-    // Drain the tail's zero-fill DMAs before anything else uses the ring.
-    wait_vmcnt<0>();
-    pad_acc();
-    if constexpr (kPairs) {
-      if (b + 1 == flush_blk) {
-        publish();
-        pad_acc();
-      }
-    }
-   }
-  };
-
   // Steps [s_begin, s_end) of sparse block-row `srow` whose entries start at
   // entry0 (entry e covers steps e*kStepsPerBlock ..). The (k-block, storage
   // block) list is staged into LDS in chunks of kIndexChunk entries.
@@ -2218,7 +1412,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     }
     int2 rows;
     int e_h, n_h, e_l, n_l;
-    if ((Cfg::kStagger || Cfg::kFlat) && R < 64) {
+    if (Cfg::kStagger && R < 64) {
       const RowPick rp = rank_rows_wave(pi, R - 1 - pi);
       rows = make_int2(rp.row_a, rp.row_b);
       e_h = rp.e_a; n_h = rp.n_a; e_l = rp.e_b; n_l = rp.n_b;
@@ -2415,7 +1609,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       j0 = panel * kBN;
       srow = target;
       if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
-        if ((Cfg::kStagger || Cfg::kFlat) && p.num_rows < 64) {
+        if (Cfg::kStagger && p.num_rows < 64) {
           const RowPick rp = rank_rows_wave(target, target);
           srow = rp.row_a;
           entry0 = rp.e_a;
@@ -2453,13 +1647,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
     // needs 12 more address registers than it has and spills; those two
     // keep the per-step pipeline.)
-    if constexpr (Cfg::kSplit)
-      pipeline_split(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
-                     p_flush > 0 ? p_flush / kStepsPerBlock : -1);
-    else if constexpr (Cfg::kFlat)
-      pipeline_flat(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
-                    p_flush > 0 ? p_flush / kStepsPerBlock : -1);
-    else if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
+    if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
                        kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
       pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
                       p_flush > 0 ? p_flush / kStepsPerBlock : -1);

@@ -29,7 +29,8 @@
 
 namespace sputnik_amd {
 
-// Experiment builds (SPUTNIK_EXP & 128) copy this into GemmParams::debug.
+// Experiment builds (SPUTNIK_EXP & 128 / 512) copy this into
+// GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
 
 // Compute units of a device, queried once per device (every SDD and every
@@ -94,7 +95,7 @@ static bool PairsEnabled() {
 #endif
 static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair = 0;
-  if (!(CfgSparse::kStagger || CfgSparse::kFlat) || CfgSparse::kWGs != 1)
+  if (!CfgSparse::kStagger || CfgSparse::kWGs != 1)
     return;
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
@@ -240,10 +241,6 @@ Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
       ta ? static_cast<const int *>(a.block_offsets) : nullptr;
   p->d_data = static_cast<const char *>(b.data);
   p->d_ld = (long long)s.ldb * 2;
-#if SPUTNIK_EXP != 0
-  // Experiment builds only: pad B's row stride (the caller allocates it).
-  if (const char *e = std::getenv("SPUTNIK_AMD_EXP_LDPAD")) p->d_ld += std::atoi(e);
-#endif
   p->c_data = static_cast<char *>(c.data);
   p->c_ld = (long long)s.ldc * 2;
   p->num_rows = s.m / kBM;
@@ -898,7 +895,7 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 }  // namespace sputnik_amd
 
 // Experiment hook (not part of include/sputnik_amd.h): per-segment cycle
-// sums of SPUTNIK_EXP & 128 builds.
+// sums / timelines of SPUTNIK_EXP & 128 / 512 builds.
 extern "C" void sputnik_exp_set_debug(void *buffer) {
   sputnik_amd::g_debug = static_cast<unsigned long long *>(buffer);
 }
