@@ -27,6 +27,8 @@ matmul the device Transpose runs inside every DSD TN/TT and DDS NN/TN step)
 and transpose (the device Transpose alone).
 
 Extra JSON objects: "roofline" (dominant kernel vs its MFMA or HBM roof),
+"dense_anchor" (torch.matmul -> hipBLASLt on a dense GEMM of the same FLOPs,
+timed beside it: what this GPU's matrix cores reach under the same clocks),
 "cpu_baseline" (the CPU oracle on a bounded sample, 1 thread and all
 allotted threads, rank 0 at N=1), "config1" (BASELINE config 1: the host
 reference matmul at 512^3, 50%), "build" (library source hash vs the tree).
@@ -432,6 +434,7 @@ class PairProblem:
         sp.Transpose(self.C)
         self.dim, self.nb = dim, nb
         self.flops = 2.0 * nz * dim * 2
+        self.anchor_shape = (dim, dim, int(round(dim * density)))
         self.bytes = 2 * (nz * 2 + 2 * dim * dim * 2) + nb * 8
         self.dtype_code = 0 if dtype == "f16" else 1
         self.desc = (f"SDD(x,w)->C then DDS(g,C) block=128 M=K=N={dim} "
@@ -543,6 +546,7 @@ class OpProblem:
             sp.RowIndices(self.S, self.S.row_indices)
         self.op, self.ta, self.tb, self.api = op, ta, tb, args.api
         self.flops = 2.0 * nz * d
+        self.anchor_shape = (d, d, int(round(d * dens)))
         meta_t = (op == "dsd" and ta) or (op == "dds" and not tb)
         meta = (d // BLOCK + 1) * 4 + nb * (6 if meta_t else 2)
         self.bytes = (nz * 2 + meta + d * d * 2 * (2 if op == "sdd" else 1) +
@@ -644,6 +648,7 @@ def run_other(args, world, rank, device, build):
                      f"of 1024 (shard_rows_by_nnz over {world})")
         metric = "effective TFLOP/s (nnz-FLOPs) row-panel DSD M=131072 K=N=4096 2%"
         scaling = "strong"
+        prob.anchor_shape = (prob.m, args.n, int(round(args.k * 0.02)))
     fn = prob.launcher()
     ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
     per = ms / args.steps
@@ -655,6 +660,14 @@ def run_other(args, world, rank, device, build):
         value, unit, hib = flops_all / (per * 1e-3) / 1e12, "TFLOP/s", True
         extra["roofline"] = roofline(prob.flops, prob.bytes, per * 1e-3,
                                      getattr(prob, "kernel", "block_gemm_kernel"))
+        shape = getattr(prob, "anchor_shape", None)
+        if rank == 0 and shape is not None:
+            anchor = dense_anchor(*shape, getattr(prob, "dtype_name", args.dtype),
+                                  device)
+            if "tflops" in anchor:
+                anchor["sparse_over_dense"] = round(
+                    value / world / anchor["tflops"], 3)
+            extra["dense_anchor"] = anchor
     if args.workload == "panel" and world > 1:
         # Optional gather of the dense result (config 5): reported beside the
         # hot path, never inside it. Equal-size panels of the padded maximum.
@@ -754,9 +767,12 @@ def main():
     # step, so the event-timed average over the K launches is its duration.
     prob, per_step, tflops, roof = head
 
-    anchor = dense_anchor(prob, args, device) if rank == 0 else None
-    if anchor:
-        anchor["dsd_over_dense"] = round(tflops / world / anchor["tflops"], 3)
+    anchor = None
+    if rank == 0:
+        kd = max(BLOCK, int(round(args.k * args.density / BLOCK)) * BLOCK)
+        anchor = dense_anchor(args.m, args.n, kd, args.dtype, device)
+        if "tflops" in anchor:
+            anchor["sparse_over_dense"] = round(tflops / world / anchor["tflops"], 3)
 
     cpu = None
     config1 = None
@@ -803,17 +819,16 @@ def main():
         dist.destroy_process_group()
 
 
-def dense_anchor(prob, args, device, iters=50):
+def dense_anchor(m, n, kd, dtype, device, iters=50):
     """The vendor dense GEMM (torch.matmul -> hipBLASLt) on the same FLOPs:
-    M x N x (K * density), random normal data, timed like the DSD steps. The
-    MFMA peak is a spec number; this is what a dense GEMM reaches on this
-    GPU under the same clocks and power draw."""
+    m x n x kd (kd = K x density), random normal data, timed like the sparse
+    steps. The MFMA peak is a spec number; this is what a dense GEMM reaches
+    on this GPU under the same clocks and power draw."""
     import torch
-    dt = torch.float16 if args.dtype == "f16" else torch.bfloat16
-    kd = max(BLOCK, int(round(args.k * args.density / BLOCK)) * BLOCK)
+    dt = torch.float16 if dtype == "f16" else torch.bfloat16
     try:
-        a = torch.randn(args.m, kd, dtype=dt, device=device)
-        b = torch.randn(kd, args.n, dtype=dt, device=device)
+        a = torch.randn(m, kd, dtype=dt, device=device)
+        b = torch.randn(kd, n, dtype=dt, device=device)
         for _ in range(10):
             torch.matmul(a, b)
         torch.cuda.synchronize()
@@ -831,8 +846,8 @@ def dense_anchor(prob, args, device, iters=50):
         return {"error": str(exc)[:200]}
     ms = sorted(times)[len(times) // 2]
     return {"op": "torch.matmul (hipBLASLt)",
-            "shape": [args.m, args.n, kd], "us": round(ms * 1e3, 2),
-            "tflops": round(2.0 * args.m * args.n * kd / (ms * 1e-3) / 1e12, 1)}
+            "shape": [m, n, kd], "us": round(ms * 1e3, 2),
+            "tflops": round(2.0 * m * n * kd / (ms * 1e-3) / 1e12, 1)}
 
 
 if __name__ == "__main__":
