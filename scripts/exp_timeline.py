@@ -59,6 +59,10 @@ def summarize(buf, wgs):
     seg = {
         "start": us(t[:, 0] - t0),
         "setup": us(t[:, 1] - t[:, 0]),
+        "to_pairs": us(t[:, 11] - t[:, 0]),
+        "offsets_load": us(np.where(t[:, 13] > 0, t[:, 13] - t[:, 11], 0)),
+        "rank": us(np.where(t[:, 12] > 0, t[:, 12] - t[:, 13], 0)),
+        "after_rank": us(np.where(t[:, 12] > 0, t[:, 1] - t[:, 12], 0)),
         "pipeline": us(t[:, 2] - t[:, 1]),
         "collect": us(t[:, 3] - t[:, 2]),
         "write": us(t[:, 4] - t[:, 3]),

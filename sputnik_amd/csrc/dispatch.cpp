@@ -489,12 +489,19 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   if (hipGetDevice(&dev) != hipSuccess) return false;
   const int cus = DeviceCUs(dev);
   if (cus <= 0) return false;
-  // Below ~6 blocks per CU the k-split block tile is faster (SDD 8192^2 x
-  // 8192, scripts/exp_grp.sh: 4 per CU 320 vs 367 us grouped; 8 per CU
-  // 656 vs 577 us).
-  constexpr int kGroupedMinPerCu = 6;
+  // From 5 blocks per CU the grouped tile is faster (SDD 8192^2 x 8192,
+  // scripts/exp_grp.sh, r02: 4 per CU k-split 318 vs grouped 362 us; 5 per
+  // CU 399 vs 365; 6 per CU 491 vs 387; 8 per CU 652 vs 570).
+  // SPUTNIK_AMD_GROUPED_MIN_PER_CU moves the switch (tuning only; never
+  // below kGrp, so a grouped grid still fills every CU).
+  constexpr int kGroupedMinPerCu = 5;
   static_assert(kGroupedMinPerCu >= kGrp, "a grouped grid fills every CU");
-  if (blocks < kGroupedMinPerCu * cus || p->num_rows > kMaxGroupRows)
+  static const int min_per_cu = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_GROUPED_MIN_PER_CU");
+    const int v = e != nullptr ? std::atoi(e) : kGroupedMinPerCu;
+    return v < kGrp ? kGrp : v;
+  }();
+  if (blocks < min_per_cu * cus || p->num_rows > kMaxGroupRows)
     return false;
   // D lane offsets: k-contiguous D gathers whole rows (n * ldb); otherwise
   // one 32-row k panel plus any column.

@@ -387,14 +387,17 @@ def test_sdd_ragged_k(k):
 @pytest.mark.parametrize("k", [200, 1024])
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
 def test_sdd_grouped_tiles(k, dtype):
-    """Enough output blocks (>= 4 per CU) for the grouped SDD tiles: up to 4
-    consecutive stored blocks of a block-row per workgroup, rows whose block
-    counts are not multiples of 4, unordered columns, a K tail, all four
-    transposes; every block against the oracle."""
-    m, n = 4096, 8192
+    """Enough output blocks (5 x CUs + 37, dispatch.cpp UseGroupedSdd) for
+    the grouped SDD tiles: up to 4 consecutive stored blocks of a block-row
+    per workgroup, rows whose block counts are not multiples of 4, unordered
+    columns, a K tail, all four transposes; every block against the oracle.
+    (test_gpu_kat.py asserts the plan at the same threshold.)"""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nb = 5 * cus + 37
+    m, n = 4096, 128 * max(64, -(-nb * 2 // 32))  # <= half of the block slots
     for ta in (False, True):
         for tb in (False, True):
-            p = dict(m=m, k=k, n=n, nonzeros=1201 * 16384, ta=ta, tb=tb,
+            p = dict(m=m, k=k, n=n, nonzeros=nb * 16384, ta=ta, tb=tb,
                      unordered=True)
             gpu, ref = run_sdd(p, dtype=dtype, seed=k + 2 * ta + tb)
             H.assert_close(gpu, ref, dtype, f"sdd-grouped {ta}{tb} k={k}")
