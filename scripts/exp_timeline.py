@@ -29,6 +29,13 @@ def topo(density, seed=0):
 def launcher(name, device):
     L = sp.lib()
     stream = torch.cuda.current_stream().cuda_stream
+    if name == "panel":  # BASELINE config 5 on one GPU: M = 131072, 2%
+        nz = mu.nonzeros_for_density(131072, 4096, 0.02)
+        off, idx = mu.random_topology(1024, 32, nz // (128 * 128),
+                                      np.random.default_rng(5))
+        prob = bench.DsdProblem(131072, 4096, off, idx, 4096, False, False,
+                                "f16", 0, device)
+        return prob, prob.launcher()
     if name.startswith("dsd"):
         off, idx = topo(int(name[3:]) / 100)
         prob = bench.DsdProblem(4096, 4096, off, idx, 4096, False, False,
@@ -96,7 +103,31 @@ def summarize(buf, wgs):
         out_pairs = None
     out["steps"] = {"mean": round(float(steps.mean()), 1),
                     "max": int(steps.max())}
+    dur = seg["end"] - seg["start"]
+    out["by_steps"] = {}
+    for lo, hi in ((0, 0), (1, 4), (5, 8), (9, 10 ** 9)):
+        sel = (steps >= lo) & (steps <= hi)
+        if sel.any():
+            out["by_steps"][f"{lo}-{hi}"] = {
+                "n": int(sel.sum()),
+                "dur_p50": round(float(np.median(dur[sel])), 2),
+                "setup_p50": round(float(np.median(seg["setup"][sel])), 2),
+                "pipe_p50": round(float(np.median(seg["pipeline"][sel])), 2),
+                "write_p50": round(float(np.median(seg["write"][sel])), 2)}
+    out["busy_us_total"] = round(float(dur.sum()), 1)
+    # Workgroups resident over time (10 buckets of the span).
+    span = float(seg["end"].max())
+    edges = np.linspace(0, span, 11)
+    conc = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        mid = (a + b) / 2
+        conc.append(int(((seg["start"] <= mid) & (seg["end"] > mid)).sum()))
+    out["resident_over_time"] = conc
     out["roles"] = {str(r): int((role == r).sum()) for r in (0, 1, 2)}
+    out["end_by_role"] = {
+        str(r): {"p50": round(float(np.median(seg["end"][role == r])), 2),
+                 "max": round(float(seg["end"][role == r].max()), 2)}
+        for r in (0, 1, 2) if (role == r).any()}
     out["pairs"] = out_pairs
     slow = int(np.argmax(seg["end"]))
     out["last_wg"] = {k: round(float(v[slow]), 2) for k, v in seg.items()}
@@ -111,7 +142,7 @@ def main():
     torch.cuda.set_device(device)
     L = sp.lib()
     L.sputnik_exp_set_debug.argtypes = [ctypes.c_void_p]
-    buf = torch.zeros(16 * 8192, dtype=torch.int64, device=device)
+    buf = torch.zeros(16 * 32768, dtype=torch.int64, device=device)
     L.sputnik_exp_set_debug(ctypes.c_void_p(buf.data_ptr()))
     for name in names:
         keep, fn = launcher(name, device)
@@ -122,7 +153,7 @@ def main():
         torch.cuda.synchronize()
         fn()
         torch.cuda.synchronize()
-        res = summarize(buf.cpu().numpy(), 8192)
+        res = summarize(buf.cpu().numpy(), 32768)
         res["workload"] = name
         print(json.dumps(res), flush=True)
         del keep

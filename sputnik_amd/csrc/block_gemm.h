@@ -126,6 +126,17 @@ struct GemmParams {
   int j_limit;                 // dense extent (elements) of the j dimension
   int k_limit;                 // SDD: K (elements)
   int num_tiles;               // output tiles (one-tile-per-workgroup grid)
+  // Persistent launch (tall DSD / DDS, dispatch.cpp UseTall): `grid`
+  // workgroups, each running tiles blockIdx.x, + tile_stride, ... <
+  // num_tiles back to back (0: one tile per workgroup, grid = num_tiles).
+  int grid;
+  int tile_stride;
+  // Persistent launches fetch their tiles past the first `grid` from this
+  // counter (one atomic per tile, issued a tile ahead): tile = grid +
+  // (fetched - tile_base). The host advances tile_base by num_tiles per
+  // launch, exactly the launch's fetches, so the counter is never reset.
+  unsigned long long *tile_counter;
+  unsigned long long tile_base;
   // Pair balancing (staggered one-workgroup-per-CU configs, see the
   // kernel): the block-rows of each panel are paired heaviest-with-lightest;
   // the light workgroup also computes the head of the heavy row and hands it
@@ -1386,6 +1397,19 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // Every branch below only sets up (srow, j0, the index segments, the step
   // range); the pipeline is then entered from ONE call site per kernel, so
   // it is inlined and the accumulators stay in registers.
+  // A persistent workgroup (p.tile_stride > 0) loops over its tiles here;
+  // the body still enters the pipeline from one call site.
+  // (Only the non-staggered DSD / DDS configs run persistent: CfgTall.)
+  constexpr bool kPersist = !Cfg::kStagger && !kSparseOut && !kSparseD;
+  int tile_next = blockIdx.x;
+  for (int iter = 0;; ++iter) {
+  // The tile after this one: fetched now, used after this tile's epilogue,
+  // so the atomic's round trip hides under the tile.
+  int fetched = 0;
+  if constexpr (kPersist) {
+    if (p.tile_stride > 0 && tid == 0)
+      fetched = (int)(atomicAdd(p.tile_counter, 1ull) - p.tile_base);
+  }
   long long out_block = 0;
   int entry0 = 0, entries = 0;   // sparse S: the row's CSR entry range
   int p_first = 0, p_steps = 0;  // scalar-index pipeline range
@@ -1453,6 +1477,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
 #define SPUTNIK_MIN_HANDOFF 2
 #endif
     constexpr int kMinHandoff = SPUTNIK_MIN_HANDOFF;
+    // (Shifting a block from the consumer to the producer to cover the
+    // consumer's collect: 50% / 90% +0 / +1%, 10% / 20% -6%; r02, not kept.)
     int hb = role == 1 ? 0 : n_h - pair_target;
     if (hb < kMinHandoff) hb = 0;
     pair_id = panel * half + pi;
@@ -1474,8 +1500,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     }
   } else {
     // ==== one output tile per workgroup ===================================
-    const int tile = (SPUTNIK_EXP & 8) ? (int)blockIdx.x
-                                       : xcd_tile(blockIdx.x, gridDim.x);
+    const int tile = kPersist && p.tile_stride > 0 ? tile_next
+                     : (SPUTNIK_EXP & 8) ? (int)blockIdx.x
+                                         : xcd_tile(blockIdx.x, gridDim.x);
     if constexpr (kGroupedSdd) {
       // Tile t = group t of the row-major list of groups, a block-row
       // contributing ceil(n_r / kGrp) groups of consecutive stored blocks.
@@ -1696,7 +1723,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       unsigned long long v = 0;
 #pragma unroll
       for (int i = 0; i < 7; ++i) v = lane == i ? tl_stamp[i] : v;
-      if (lane == 7) v = (unsigned long long)p_steps;
+      if (lane == 7)
+        v = (unsigned long long)(p_steps ? p_steps : entries * kStepsPerBlock);
       if (lane == 8)
         v = (unsigned long long)(do_collect ? 2 : (p_flush > 0 ? 1 : 0));
       if (lane == 9) v = (unsigned long long)srow;
@@ -1715,6 +1743,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       for (int q = 0; q < 6; ++q) o[q] = seg_sum[q];
     }
   }
+  if (!kPersist || p.tile_stride <= 0) break;
+  // Slot iter & 1: its next write (two tiles on) comes after the barrier
+  // that ends the next tile, when every wave has read it.
+  if (tid == 0) scratch[iter & 1] = min(p.grid + fetched, p.num_tiles);
+  __syncthreads();  // the next tile reuses the ring and the staging image
+  tile_next = __builtin_amdgcn_readfirstlane(scratch[iter & 1]);
+  if (tile_next >= p.num_tiles) break;
+  }  // tiles of a persistent workgroup
 #undef SEG_STAMP
 #undef SEG_ACCUM
 }

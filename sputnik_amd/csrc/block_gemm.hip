@@ -14,7 +14,8 @@ template <typename T, bool kSparseOut, bool kSKC, bool kDKC, bool kOutT,
           class Cfg>
 hipError_t LaunchCfg(const GemmParams &p, hipStream_t stream) {
   hipLaunchKernelGGL((block_gemm_kernel<T, kSparseOut, kSKC, kDKC, kOutT, Cfg>),
-                     dim3(p.num_tiles), dim3(64 * Cfg::kWaves), 0,
+                     dim3(p.grid > 0 ? p.grid : p.num_tiles),
+                     dim3(64 * Cfg::kWaves), 0,
                      stream, p);
   return hipGetLastError();
 }

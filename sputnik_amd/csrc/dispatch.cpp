@@ -73,6 +73,17 @@ static PairSlot g_pairs[kMaxPairSlots];
 static std::mutex g_pairs_mu;
 static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
 
+// Tile counter of persistent tall launches, per (device, stream): each
+// launch makes exactly num_tiles fetches, so the host advances `base` and the
+// counter is never reset (stream order; not used under graph capture).
+struct CounterSlot {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  unsigned long long *counter = nullptr;
+  unsigned long long base = 0;
+};
+static CounterSlot g_counters[kMaxPairSlots];
+
 static bool PairsEnabled() {
 #ifdef SPUTNIK_NO_PAIRS
   return false;
@@ -516,7 +527,7 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
 // Tall sparse operands (more block-rows than the in-kernel row ranking
 // handles, so no LPT order and no pair balancing) have many more tiles than
 // CUs: they run on CfgTall, two workgroups per CU.
-bool UseTall(GemmParams *p) {
+bool UseTall(GemmParams *p, hipStream_t stream) {
   // SPUTNIK_AMD_TALL: 0 never, 2 always (experiments), unset: tall only.
   static const int mode = [] {
     const char *e = std::getenv("SPUTNIK_AMD_TALL");
@@ -533,6 +544,54 @@ bool UseTall(GemmParams *p) {
   }
   p->num_jtiles = (p->j_limit + CfgTall::kBN - 1) / CfgTall::kBN;
   p->num_tiles = p->num_rows * p->num_jtiles;
+  // Persistent: one workgroup per slot; the first `slots` tiles go by
+  // workgroup index, the rest are fetched from a per-stream counter. Short
+  // tiles (most rows of a tall 2% operand hold 0-2 blocks) otherwise leave
+  // ~20% of the slots idle between a workgroup's end and the next dispatch
+  // (r02 timeline: 400-460 of 512 resident); a static tile stride instead
+  // loses more to imbalance (403 vs 337 us, config 5).
+  static const int persistent = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_TALL_PERSISTENT");
+    return e != nullptr ? std::atoi(e) : 1;
+  }();
+  int dev = 0;
+  const int cus = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
+  const int slots = cus * CfgTall::kWGs;
+  if (!persistent || slots <= 0 || p->num_tiles <= slots) return true;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
+      cs != hipStreamCaptureStatusNone)
+    return true;  // host-side counter base: not replayable
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  CounterSlot *slot = nullptr;
+  for (auto &c : g_counters)
+    if (c.counter != nullptr && c.device == dev && c.stream == stream) {
+      slot = &c;
+      break;
+    }
+  if (slot == nullptr) {
+    for (auto &c : g_counters)
+      if (c.counter == nullptr) {
+        slot = &c;
+        break;
+      }
+    if (slot == nullptr) return true;
+    unsigned long long *ctr = nullptr;
+    if (hipMalloc(&ctr, sizeof(*ctr)) != hipSuccess) return true;
+    if (hipMemset(ctr, 0, sizeof(*ctr)) != hipSuccess) {
+      (void)hipFree(ctr);
+      return true;
+    }
+    slot->device = dev;
+    slot->stream = stream;
+    slot->counter = ctr;
+    slot->base = 0;
+  }
+  p->grid = slots;
+  p->tile_stride = slots;
+  p->tile_counter = slot->counter;
+  p->tile_base = slot->base;
+  slot->base += (unsigned long long)p->num_tiles;  // this launch's fetches
   return true;
 }
 
@@ -554,7 +613,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
-  const bool tall = UseTall(&p);
+  const bool tall = UseTall(&p, stream);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 
@@ -572,7 +631,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, b.nonzeros / (kBlock * kBlock), stream);
-  const bool tall = UseTall(&p);
+  const bool tall = UseTall(&p, stream);
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);
 }
