@@ -137,6 +137,28 @@ def test_kat_dsd_ex_tall(ta, tb):
     _equal(got, want, f"dsd tall {ta}{tb}")
 
 
+def test_kat_tall_persistent_repeated():
+    """Tall DSD with many more tiles than workgroup slots runs persistent
+    (tiles past the first grid fetched from a per-stream counter whose base
+    the host advances per launch, dispatch.cpp UseTall): repeated launches on
+    one stream, interleaved with launches on a second stream, all exact."""
+    rng = np.random.default_rng(11)
+    A = ISparse(65536, 256, 0.3, rng, "f16")
+    Bd = IDense(256, 1000, rng, "f16")  # 4 tiles of 256 columns, the last partial
+    want = _expect(A.dense.astype(np.float64) @ Bd.values, "f16")
+    s2 = torch.cuda.Stream()
+    for i, stream in enumerate([None, None, s2, None, s2, s2, None]):
+        C, c_t = _nan_out(65536, 1000, "f16")
+        if stream is None:
+            sp.Matmul(A.m, False, Bd.m, False, C)
+        else:
+            stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(stream):
+                sp.Matmul(A.m, False, Bd.m, False, C)
+            stream.synchronize()
+        _equal(c_t, want, f"tall persistent launch {i}")
+
+
 @pytest.mark.parametrize("ta", [False, True])
 def test_kat_dsd_4096_pairs(ta):
     """BASELINE config 2 shape (4096^3, 50%): one tile per CU, the
