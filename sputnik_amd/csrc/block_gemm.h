@@ -1403,353 +1403,353 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr bool kPersist = !Cfg::kStagger && !kSparseOut && !kSparseD;
   int tile_next = blockIdx.x;
   for (int iter = 0;; ++iter) {
-  // The tile after this one: fetched now, used after this tile's epilogue,
-  // so the atomic's round trip hides under the tile.
-  int fetched = 0;
-  if constexpr (kPersist) {
-    if (p.tile_stride > 0 && tid == 0)
-      fetched = (int)(atomicAdd(p.tile_counter, 1ull) - p.tile_base);
-  }
-  long long out_block = 0;
-  int entry0 = 0, entries = 0;   // sparse S: the row's CSR entry range
-  int p_first = 0, p_steps = 0;  // scalar-index pipeline range
-  int p_flush = -1;              // pair producer: end of the head segment
-  bool do_collect = false;       // pair consumer
-  bool use_pairs = false;
-  if constexpr (kPairs) use_pairs = p.pair != 0;
-  tl(7);
-  if (use_pairs) {
-    // ==== pair balancing (one workgroup per CU, #tiles <= #CUs) ==========
-    // A tile's length is its block-row's nonzero count, and with one tile
-    // per CU the launch ends with the longest row. Within each panel the
-    // rows are paired by rank, i <-> R-1-i: the heavy row (rank i, n_h
-    // blocks) gives its first hb = (n_h - n_l) / 2 blocks to the light row's
-    // workgroup (n_l blocks), which runs them first in the same pipeline,
-    // publishes the fp32 partial and then runs its own row; the heavy
-    // workgroup runs blocks [hb, n_h) and adds the partial. Both run
-    // (n_h + n_l) / 2 blocks, +-1. Grid order: [light x P*(R/2)] [middle row
-    // of odd R x P] [heavy x P*(R/2)], so a producer always precedes its
-    // consumer in dispatch order and never waits; pairs share an XCD when
-    // P*(R/2) + P*(R&1) is a multiple of 8.
-    const int R = p.num_rows;
-    const int half = R >> 1;
-    const int n_light = p.num_jtiles * half;
-    const int n_solo = p.num_jtiles * (R & 1);
-    const int bid = blockIdx.x;
-    int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
-    if (bid < n_light) {
-      role = 0;
-      const int t = xcd_tile(bid, n_light);
-      panel = t / half;
-      pi = t % half;
-    } else if (bid < n_light + n_solo) {
-      role = 1;
-      panel = bid - n_light;
-      pi = half;
-    } else {
-      role = 2;
-      const int t = xcd_tile(bid - n_light - n_solo, n_light);
-      panel = t / half;
-      pi = t % half;
+    // The tile after this one: fetched now, used after this tile's epilogue,
+    // so the atomic's round trip hides under the tile.
+    int fetched = 0;
+    if constexpr (kPersist) {
+      if (p.tile_stride > 0 && tid == 0)
+        fetched = (int)(atomicAdd(p.tile_counter, 1ull) - p.tile_base);
     }
-    int2 rows;
-    int e_h, n_h, e_l, n_l;
-    if (Cfg::kStagger && R < 64) {
-      const RowPick rp = rank_rows_wave(pi, R - 1 - pi);
-      tl(8);
-      rows = make_int2(rp.row_a, rp.row_b);
-      e_h = rp.e_a; n_h = rp.n_a; e_l = rp.e_b; n_l = rp.n_b;
-    } else {
-      rows = rank_rows(pi, R - 1 - pi);
-      // The offsets are still staged in LDS by rank_rows (the ring is not
-      // written before the first DMA): no dependent global round trip.
-      const int *offs = reinterpret_cast<const int *>(lds);
-      e_h = __builtin_amdgcn_readfirstlane(offs[rows.x]);
-      n_h = __builtin_amdgcn_readfirstlane(offs[rows.x + 1]) - e_h;
-      e_l = __builtin_amdgcn_readfirstlane(offs[rows.y]);
-      n_l = __builtin_amdgcn_readfirstlane(offs[rows.y + 1]) - e_l;
-      __syncthreads();  // staged offsets / scratch read by every wave
-    }
-    // Hand over only what exceeds the panel's balanced target, and nothing
-    // under kMinHandoff blocks: a hand-off costs each side about one
-    // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
-#ifndef SPUTNIK_MIN_HANDOFF
-#define SPUTNIK_MIN_HANDOFF 2
-#endif
-    constexpr int kMinHandoff = SPUTNIK_MIN_HANDOFF;
-    // (Shifting a block from the consumer to the producer to cover the
-    // consumer's collect: 50% / 90% +0 / +1%, 10% / 20% -6%; r02, not kept.)
-    int hb = role == 1 ? 0 : n_h - pair_target;
-    if (hb < kMinHandoff) hb = 0;
-    pair_id = panel * half + pi;
-    j0 = panel * kBN;
-    if (role == 0) {
-      srow = rows.y;
-      idx_base = e_h;
-      idx_split = hb;
-      idx_base2 = e_l;
-      p_first = 0;
-      p_steps = (hb + n_l) * kStepsPerBlock;
-      p_flush = hb > 0 ? hb * kStepsPerBlock : -1;
-    } else {
-      srow = rows.x;
-      idx_base = e_h;
-      p_first = hb * kStepsPerBlock;
-      p_steps = (n_h - hb) * kStepsPerBlock;
-      do_collect = hb > 0;
-    }
-  } else {
-    // ==== one output tile per workgroup ===================================
-    const int tile = kPersist && p.tile_stride > 0 ? tile_next
-                     : (SPUTNIK_EXP & 8) ? (int)blockIdx.x
-                                         : xcd_tile(blockIdx.x, gridDim.x);
-    if constexpr (kGroupedSdd) {
-      // Tile t = group t of the row-major list of groups, a block-row
-      // contributing ceil(n_r / kGrp) groups of consecutive stored blocks.
-      // One parallel scan of the group counts over C's offsets (each lane a
-      // contiguous run of rows; wave scan by shuffles, then wave totals); the
-      // grid is the host's upper bound nb/kGrp + R, so late tiles exit.
+    long long out_block = 0;
+    int entry0 = 0, entries = 0;   // sparse S: the row's CSR entry range
+    int p_first = 0, p_steps = 0;  // scalar-index pipeline range
+    int p_flush = -1;              // pair producer: end of the head segment
+    bool do_collect = false;       // pair consumer
+    bool use_pairs = false;
+    if constexpr (kPairs) use_pairs = p.pair != 0;
+    tl(7);
+    if (use_pairs) {
+      // ==== pair balancing (one workgroup per CU, #tiles <= #CUs) ==========
+      // A tile's length is its block-row's nonzero count, and with one tile
+      // per CU the launch ends with the longest row. Within each panel the
+      // rows are paired by rank, i <-> R-1-i: the heavy row (rank i, n_h
+      // blocks) gives its first hb = (n_h - n_l) / 2 blocks to the light row's
+      // workgroup (n_l blocks), which runs them first in the same pipeline,
+      // publishes the fp32 partial and then runs its own row; the heavy
+      // workgroup runs blocks [hb, n_h) and adds the partial. Both run
+      // (n_h + n_l) / 2 blocks, +-1. Grid order: [light x P*(R/2)] [middle row
+      // of odd R x P] [heavy x P*(R/2)], so a producer always precedes its
+      // consumer in dispatch order and never waits; pairs share an XCD when
+      // P*(R/2) + P*(R&1) is a multiple of 8.
       const int R = p.num_rows;
-      const int per = (R + kThreads - 1) / kThreads;
-      const int r0 = min(R, tid * per), r1 = min(R, r0 + per);
-      int local = 0;
-      for (int r = r0; r < r1; ++r)
-        local += (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
-      int incl = local;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += v;
+      const int half = R >> 1;
+      const int n_light = p.num_jtiles * half;
+      const int n_solo = p.num_jtiles * (R & 1);
+      const int bid = blockIdx.x;
+      int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
+      if (bid < n_light) {
+        role = 0;
+        const int t = xcd_tile(bid, n_light);
+        panel = t / half;
+        pi = t % half;
+      } else if (bid < n_light + n_solo) {
+        role = 1;
+        panel = bid - n_light;
+        pi = half;
+      } else {
+        role = 2;
+        const int t = xcd_tile(bid - n_light - n_solo, n_light);
+        panel = t / half;
+        pi = t % half;
       }
-      // Row group counts' min / max: when every row has the same count G
-      // (block-rows sharing one column set, e.g. the MoE expert-diagonal),
-      // tiles run group-major (t -> group t / R, row t % R), so the
-      // workgroups that run together on an XCD share one D column slice in
-      // its L2 instead of each streaming a different one from HBM.
-      int gmin = 0x7fffffff, gmax = 0;
-      for (int r = r0; r < r1; ++r) {
-        const int g =
-            (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
-        gmin = min(gmin, g);
-        gmax = max(gmax, g);
+      int2 rows;
+      int e_h, n_h, e_l, n_l;
+      if (Cfg::kStagger && R < 64) {
+        const RowPick rp = rank_rows_wave(pi, R - 1 - pi);
+        tl(8);
+        rows = make_int2(rp.row_a, rp.row_b);
+        e_h = rp.e_a; n_h = rp.n_a; e_l = rp.e_b; n_l = rp.n_b;
+      } else {
+        rows = rank_rows(pi, R - 1 - pi);
+        // The offsets are still staged in LDS by rank_rows (the ring is not
+        // written before the first DMA): no dependent global round trip.
+        const int *offs = reinterpret_cast<const int *>(lds);
+        e_h = __builtin_amdgcn_readfirstlane(offs[rows.x]);
+        n_h = __builtin_amdgcn_readfirstlane(offs[rows.x + 1]) - e_h;
+        e_l = __builtin_amdgcn_readfirstlane(offs[rows.y]);
+        n_l = __builtin_amdgcn_readfirstlane(offs[rows.y + 1]) - e_l;
+        __syncthreads();  // staged offsets / scratch read by every wave
       }
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        gmin = min(gmin, __shfl_xor(gmin, d, 64));
-        gmax = max(gmax, __shfl_xor(gmax, d, 64));
+      // Hand over only what exceeds the panel's balanced target, and nothing
+      // under kMinHandoff blocks: a hand-off costs each side about one
+      // 256 KiB partial round trip beyond L2 (≈ 1-2 blocks of pipeline).
+  #ifndef SPUTNIK_MIN_HANDOFF
+  #define SPUTNIK_MIN_HANDOFF 2
+  #endif
+      constexpr int kMinHandoff = SPUTNIK_MIN_HANDOFF;
+      // (Shifting a block from the consumer to the producer to cover the
+      // consumer's collect: 50% / 90% +0 / +1%, 10% / 20% -6%; r02, not kept.)
+      int hb = role == 1 ? 0 : n_h - pair_target;
+      if (hb < kMinHandoff) hb = 0;
+      pair_id = panel * half + pi;
+      j0 = panel * kBN;
+      if (role == 0) {
+        srow = rows.y;
+        idx_base = e_h;
+        idx_split = hb;
+        idx_base2 = e_l;
+        p_first = 0;
+        p_steps = (hb + n_l) * kStepsPerBlock;
+        p_flush = hb > 0 ? hb * kStepsPerBlock : -1;
+      } else {
+        srow = rows.x;
+        idx_base = e_h;
+        p_first = hb * kStepsPerBlock;
+        p_steps = (n_h - hb) * kStepsPerBlock;
+        do_collect = hb > 0;
       }
-      int *wsum = reinterpret_cast<int *>(lds);
-      if (lane == 63) {
-        wsum[wave] = incl;
-        wsum[kNW + wave] = gmin;
-        wsum[2 * kNW + wave] = gmax;
-      }
-      __syncthreads();
-      int before = 0, total = 0;
-      for (int w2 = 0; w2 < kNW; ++w2) {
-        const int v = wsum[w2];
-        before += w2 < wave ? v : 0;
-        total += v;
-        gmin = min(gmin, wsum[kNW + w2]);
-        gmax = max(gmax, wsum[2 * kNW + w2]);
-      }
-      int start = before + incl - local;
-      const bool uniform = gmin == gmax;
-      if (!uniform) {
+    } else {
+      // ==== one output tile per workgroup ===================================
+      const int tile = kPersist && p.tile_stride > 0 ? tile_next
+                       : (SPUTNIK_EXP & 8) ? (int)blockIdx.x
+                                           : xcd_tile(blockIdx.x, gridDim.x);
+      if constexpr (kGroupedSdd) {
+        // Tile t = group t of the row-major list of groups, a block-row
+        // contributing ceil(n_r / kGrp) groups of consecutive stored blocks.
+        // One parallel scan of the group counts over C's offsets (each lane a
+        // contiguous run of rows; wave scan by shuffles, then wave totals); the
+        // grid is the host's upper bound nb/kGrp + R, so late tiles exit.
+        const int R = p.num_rows;
+        const int per = (R + kThreads - 1) / kThreads;
+        const int r0 = min(R, tid * per), r1 = min(R, r0 + per);
+        int local = 0;
+        for (int r = r0; r < r1; ++r)
+          local += (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
+        int incl = local;
+  #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int v = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += v;
+        }
+        // Row group counts' min / max: when every row has the same count G
+        // (block-rows sharing one column set, e.g. the MoE expert-diagonal),
+        // tiles run group-major (t -> group t / R, row t % R), so the
+        // workgroups that run together on an XCD share one D column slice in
+        // its L2 instead of each streaming a different one from HBM.
+        int gmin = 0x7fffffff, gmax = 0;
         for (int r = r0; r < r1; ++r) {
           const int g =
               (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
-          if (tile >= start && tile < start + g) {
-            scratch[0] = r;
-            scratch[1] = tile - start;
-          }
-          start += g;
+          gmin = min(gmin, g);
+          gmax = max(gmax, g);
         }
-      }
-      __syncthreads();
-      if (tile >= total) return;  // whole workgroup: no barrier pending
-      int gi;
-      if (uniform) {
-        srow = tile % R;
-        gi = tile / R;
-      } else {
-        srow = __builtin_amdgcn_readfirstlane(scratch[0]);
-        gi = __builtin_amdgcn_readfirstlane(scratch[1]);
-      }
-      const int b0 = p.c_offsets[srow] + gi * kGrp;
-      grp_b0 = b0;
-      grp_count = min(kGrp, p.c_offsets[srow + 1] - b0);
-      grp_c0 = p.c_indices[b0] * kBlock;
-      if (kGrp > 1 && grp_count > 1) grp_c1 = p.c_indices[b0 + 1] * kBlock;
-      if (kGrp > 2 && grp_count > 2) grp_c2 = p.c_indices[b0 + 2] * kBlock;
-      if (kGrp > 3 && grp_count > 3) grp_c3 = p.c_indices[b0 + 3] * kBlock;
-      __syncthreads();  // wsum / scratch reads done before the ring is used
-    } else if constexpr (kSparseD) {
-      // DSS tile (r, c): op(A)'s row r meets op(B)'s column c. LDS (after
-      // the ring): bmap[256] = D storage block of k-block k (or -1), then
-      // the intersection as S blocks [256] and D blocks [256], then count.
-      const int nc = p.num_jtiles;
-      srow = tile / nc;
-      const int c = tile % nc;
-      j0 = c * kBlock;
-      int *bmap = reinterpret_cast<int *>(lds + kRingBytes);
-      int *ls = bmap + kDssMaxK;
-      int *ld = ls + kDssMaxK;
-      int *cnt = ld + kDssMaxK;
-      for (int k = tid; k < kDssMaxK; k += kThreads) bmap[k] = -1;
-      __syncthreads();
-      const int b0 = p.d_offsets[c], b1 = p.d_offsets[c + 1];
-      for (int e = b0 + tid; e < b1; e += kThreads)
-        bmap[p.d_indices[e]] =
-            p.d_block_offsets != nullptr ? p.d_block_offsets[e] : e;
-      __syncthreads();
-      if (wave == 0) {  // order-preserving compaction of op(A)'s row
-        const int a0 = p.s_offsets[srow], a1 = p.s_offsets[srow + 1];
-        int pos = 0;
-        for (int base = a0; base < a1; base += 64) {
-          const int e = base + lane;
-          const bool valid = e < a1;
-          const int k = valid ? p.s_indices[e] : 0;
-          const int bm = valid ? bmap[k] : -1;
-          const bool hit = bm >= 0;
-          const unsigned long long ball = __ballot(hit);
-          if (hit) {
-            const int at = pos + __popcll(ball & ((1ull << lane) - 1));
-            ls[at] = p.s_block_offsets != nullptr ? p.s_block_offsets[e] : e;
-            ld[at] = bm;
-          }
-          pos += __popcll(ball);
+  #pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          gmin = min(gmin, __shfl_xor(gmin, d, 64));
+          gmax = max(gmax, __shfl_xor(gmax, d, 64));
         }
-        if (lane == 0) cnt[0] = pos;
-      }
-      __syncthreads();
-      entries = __builtin_amdgcn_readfirstlane(cnt[0]);
-    } else if constexpr (kSparseIn) {
-      // SSD: block (r, c) of C is row r of op(A) times column panel c of
-      // op(B). SDS computes the block transposed: row c of op(B)^T times
-      // row panel r of op(A)^T.
-      out_block = tile;
-      grp_b0 = tile;
-      const int r = p.c_row_indices[tile];
-      const int c = p.c_indices[tile];
-      srow = kOutT ? c : r;
-      j0 = (kOutT ? r : c) * kBlock;
-      entry0 = p.s_offsets[srow];
-      entries = p.s_offsets[srow + 1] - entry0;
-    } else if constexpr (kSparseOut) {
-      out_block = tile;
-      grp_b0 = tile;
-      srow = p.c_row_indices[tile];
-      j0 = p.c_indices[tile] * kBlock;
-    } else {
-      // Longest-processing-time order: within each dense panel, tile t takes
-      // the block-row with the t-th most nonzeros (ties by row index), so
-      // the workgroups dispatched last are the shortest. Snake (several
-      // workgroups per CU): odd panels run ascending, so two workgroups
-      // sharing a CU pair a long row with a short one. Rows are ranked in
-      // LDS (R <= kLptRows; taller matrices have many more tiles than CUs and
-      // keep natural order).
-      const int panel = tile / p.num_rows;
-      int target = tile % p.num_rows;
-      if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
-      j0 = panel * kBN;
-      srow = target;
-      if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
-        if (Cfg::kStagger && p.num_rows < 64) {
-          const RowPick rp = rank_rows_wave(target, target);
-          srow = rp.row_a;
-          entry0 = rp.e_a;
-          entries = rp.n_a;
+        int *wsum = reinterpret_cast<int *>(lds);
+        if (lane == 63) {
+          wsum[wave] = incl;
+          wsum[kNW + wave] = gmin;
+          wsum[2 * kNW + wave] = gmax;
+        }
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w2 = 0; w2 < kNW; ++w2) {
+          const int v = wsum[w2];
+          before += w2 < wave ? v : 0;
+          total += v;
+          gmin = min(gmin, wsum[kNW + w2]);
+          gmax = max(gmax, wsum[2 * kNW + w2]);
+        }
+        int start = before + incl - local;
+        const bool uniform = gmin == gmax;
+        if (!uniform) {
+          for (int r = r0; r < r1; ++r) {
+            const int g =
+                (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
+            if (tile >= start && tile < start + g) {
+              scratch[0] = r;
+              scratch[1] = tile - start;
+            }
+            start += g;
+          }
+        }
+        __syncthreads();
+        if (tile >= total) return;  // whole workgroup: no barrier pending
+        int gi;
+        if (uniform) {
+          srow = tile % R;
+          gi = tile / R;
         } else {
-          srow = rank_rows(target, target).x;
-          const int *offs = reinterpret_cast<const int *>(lds);  // staged
-          entry0 = __builtin_amdgcn_readfirstlane(offs[srow]);
-          entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
-          __syncthreads();  // staged offsets / scratch read by every wave
+          srow = __builtin_amdgcn_readfirstlane(scratch[0]);
+          gi = __builtin_amdgcn_readfirstlane(scratch[1]);
         }
-      } else {
+        const int b0 = p.c_offsets[srow] + gi * kGrp;
+        grp_b0 = b0;
+        grp_count = min(kGrp, p.c_offsets[srow + 1] - b0);
+        grp_c0 = p.c_indices[b0] * kBlock;
+        if (kGrp > 1 && grp_count > 1) grp_c1 = p.c_indices[b0 + 1] * kBlock;
+        if (kGrp > 2 && grp_count > 2) grp_c2 = p.c_indices[b0 + 2] * kBlock;
+        if (kGrp > 3 && grp_count > 3) grp_c3 = p.c_indices[b0 + 3] * kBlock;
+        __syncthreads();  // wsum / scratch reads done before the ring is used
+      } else if constexpr (kSparseD) {
+        // DSS tile (r, c): op(A)'s row r meets op(B)'s column c. LDS (after
+        // the ring): bmap[256] = D storage block of k-block k (or -1), then
+        // the intersection as S blocks [256] and D blocks [256], then count.
+        const int nc = p.num_jtiles;
+        srow = tile / nc;
+        const int c = tile % nc;
+        j0 = c * kBlock;
+        int *bmap = reinterpret_cast<int *>(lds + kRingBytes);
+        int *ls = bmap + kDssMaxK;
+        int *ld = ls + kDssMaxK;
+        int *cnt = ld + kDssMaxK;
+        for (int k = tid; k < kDssMaxK; k += kThreads) bmap[k] = -1;
+        __syncthreads();
+        const int b0 = p.d_offsets[c], b1 = p.d_offsets[c + 1];
+        for (int e = b0 + tid; e < b1; e += kThreads)
+          bmap[p.d_indices[e]] =
+              p.d_block_offsets != nullptr ? p.d_block_offsets[e] : e;
+        __syncthreads();
+        if (wave == 0) {  // order-preserving compaction of op(A)'s row
+          const int a0 = p.s_offsets[srow], a1 = p.s_offsets[srow + 1];
+          int pos = 0;
+          for (int base = a0; base < a1; base += 64) {
+            const int e = base + lane;
+            const bool valid = e < a1;
+            const int k = valid ? p.s_indices[e] : 0;
+            const int bm = valid ? bmap[k] : -1;
+            const bool hit = bm >= 0;
+            const unsigned long long ball = __ballot(hit);
+            if (hit) {
+              const int at = pos + __popcll(ball & ((1ull << lane) - 1));
+              ls[at] = p.s_block_offsets != nullptr ? p.s_block_offsets[e] : e;
+              ld[at] = bm;
+            }
+            pos += __popcll(ball);
+          }
+          if (lane == 0) cnt[0] = pos;
+        }
+        __syncthreads();
+        entries = __builtin_amdgcn_readfirstlane(cnt[0]);
+      } else if constexpr (kSparseIn) {
+        // SSD: block (r, c) of C is row r of op(A) times column panel c of
+        // op(B). SDS computes the block transposed: row c of op(B)^T times
+        // row panel r of op(A)^T.
+        out_block = tile;
+        grp_b0 = tile;
+        const int r = p.c_row_indices[tile];
+        const int c = p.c_indices[tile];
+        srow = kOutT ? c : r;
+        j0 = (kOutT ? r : c) * kBlock;
         entry0 = p.s_offsets[srow];
         entries = p.s_offsets[srow + 1] - entry0;
+      } else if constexpr (kSparseOut) {
+        out_block = tile;
+        grp_b0 = tile;
+        srow = p.c_row_indices[tile];
+        j0 = p.c_indices[tile] * kBlock;
+      } else {
+        // Longest-processing-time order: within each dense panel, tile t takes
+        // the block-row with the t-th most nonzeros (ties by row index), so
+        // the workgroups dispatched last are the shortest. Snake (several
+        // workgroups per CU): odd panels run ascending, so two workgroups
+        // sharing a CU pair a long row with a short one. Rows are ranked in
+        // LDS (R <= kLptRows; taller matrices have many more tiles than CUs and
+        // keep natural order).
+        const int panel = tile / p.num_rows;
+        int target = tile % p.num_rows;
+        if (Cfg::kWGs > 1 && (panel & 1)) target = p.num_rows - 1 - target;
+        j0 = panel * kBN;
+        srow = target;
+        if (!(SPUTNIK_EXP & 4) && p.num_rows <= kLptRows) {
+          if (Cfg::kStagger && p.num_rows < 64) {
+            const RowPick rp = rank_rows_wave(target, target);
+            srow = rp.row_a;
+            entry0 = rp.e_a;
+            entries = rp.n_a;
+          } else {
+            srow = rank_rows(target, target).x;
+            const int *offs = reinterpret_cast<const int *>(lds);  // staged
+            entry0 = __builtin_amdgcn_readfirstlane(offs[srow]);
+            entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
+            __syncthreads();  // staged offsets / scratch read by every wave
+          }
+        } else {
+          entry0 = p.s_offsets[srow];
+          entries = p.s_offsets[srow + 1] - entry0;
+        }
+        idx_base = entry0;
+        p_first = 0;
+        p_steps = entries * kStepsPerBlock;
       }
-      idx_base = entry0;
-      p_first = 0;
-      p_steps = entries * kStepsPerBlock;
     }
-  }
-  setup_d(j0);
-  zero_acc();
-  tl(1);
-  if constexpr (kDenseS) {
-    const int nsteps = (p.k_limit + kBK - 1) / kBK;
-    // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
-    // zeros through the k mask (at most 3, none when K % 128 == 0).
-    if constexpr (SPUTNIK_SDD_BLOCK_LOOP != 0 && Cfg::kStagger &&
-                  kStages == 4)
-      pipeline_blocks(0, (nsteps + 3) / 4, -1);
+    setup_d(j0);
+    zero_acc();
+    tl(1);
+    if constexpr (kDenseS) {
+      const int nsteps = (p.k_limit + kBK - 1) / kBK;
+      // Staggered (grouped) SDD: whole groups of 4 k-steps; steps past K read
+      // zeros through the k mask (at most 3, none when K % 128 == 0).
+      if constexpr (SPUTNIK_SDD_BLOCK_LOOP != 0 && Cfg::kStagger &&
+                    kStages == 4)
+        pipeline_blocks(0, (nsteps + 3) / 4, -1);
+      else
+        pipeline(0, nsteps);
+    } else if constexpr (kScalarIdx) {
+      cached_e = -1;
+      // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
+      // needs 12 more address registers than it has and spills; those two
+      // keep the per-step pipeline.)
+      if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
+                         kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
+        pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
+                        p_flush > 0 ? p_flush / kStepsPerBlock : -1);
+      else
+        pipeline(p_first, p_steps, p_flush);
+      tl(2);
+      if (do_collect) collect();
+    } else if constexpr (kSparseD) {
+      cached_e = -1;
+      pipeline(0, entries * kStepsPerBlock);  // list staged by the setup
+    } else {
+      run_sparse(entry0, 0, entries * kStepsPerBlock);
+    }
+    tl(3);
+    bool empty = false;
+    if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
+    if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
+    if (empty)
+      write_zero_tile();
     else
-      pipeline(0, nsteps);
-  } else if constexpr (kScalarIdx) {
-    cached_e = -1;
-    // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
-    // needs 12 more address registers than it has and spills; those two
-    // keep the per-step pipeline.)
-    if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
-                       kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
-      pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
-                      p_flush > 0 ? p_flush / kStepsPerBlock : -1);
-    else
-      pipeline(p_first, p_steps, p_flush);
-    tl(2);
-    if (do_collect) collect();
-  } else if constexpr (kSparseD) {
-    cached_e = -1;
-    pipeline(0, entries * kStepsPerBlock);  // list staged by the setup
-  } else {
-    run_sparse(entry0, 0, entries * kStepsPerBlock);
-  }
-  tl(3);
-  bool empty = false;
-  if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
-  if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
-  if (empty)
-    write_zero_tile();
-  else
-    write_tile(out_block);
-  if constexpr ((SPUTNIK_EXP & 512) != 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    tl(4);
-    if (p.debug != nullptr && wave == 0 && lane < 14) {
-      // lane i < 7 writes stamp i; then the steps, the role and the row.
-      unsigned long long v = 0;
-#pragma unroll
-      for (int i = 0; i < 7; ++i) v = lane == i ? tl_stamp[i] : v;
-      if (lane == 7)
-        v = (unsigned long long)(p_steps ? p_steps : entries * kStepsPerBlock);
-      if (lane == 8)
-        v = (unsigned long long)(do_collect ? 2 : (p_flush > 0 ? 1 : 0));
-      if (lane == 9) v = (unsigned long long)srow;
-      if (lane == 10) v = (unsigned long long)pair_id;
-      if (lane == 11) v = tl_stamp[7];
-      if (lane == 12) v = tl_stamp[8];
-      if (lane == 13) v = tl_stamp[9];
-      p.debug[blockIdx.x * 16 + lane] = v;
+      write_tile(out_block);
+    if constexpr ((SPUTNIK_EXP & 512) != 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tl(4);
+      if (p.debug != nullptr && wave == 0 && lane < 14) {
+        // lane i < 7 writes stamp i; then the steps, the role and the row.
+        unsigned long long v = 0;
+  #pragma unroll
+        for (int i = 0; i < 7; ++i) v = lane == i ? tl_stamp[i] : v;
+        if (lane == 7)
+          v = (unsigned long long)(p_steps ? p_steps : entries * kStepsPerBlock);
+        if (lane == 8)
+          v = (unsigned long long)(do_collect ? 2 : (p_flush > 0 ? 1 : 0));
+        if (lane == 9) v = (unsigned long long)srow;
+        if (lane == 10) v = (unsigned long long)pair_id;
+        if (lane == 11) v = tl_stamp[7];
+        if (lane == 12) v = tl_stamp[8];
+        if (lane == 13) v = tl_stamp[9];
+        p.debug[blockIdx.x * 16 + lane] = v;
+      }
     }
-  }
-  if constexpr ((SPUTNIK_EXP & 128) != 0) {
-    if (p.debug != nullptr && lane == 0 && (wave == 0 || wave == kNW / 2)) {
-      unsigned long long *o =
-          p.debug + 2048 * 16 + blockIdx.x * 16 + (wave == 0 ? 0 : 8);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) o[q] = seg_sum[q];
+    if constexpr ((SPUTNIK_EXP & 128) != 0) {
+      if (p.debug != nullptr && lane == 0 && (wave == 0 || wave == kNW / 2)) {
+        unsigned long long *o =
+            p.debug + 2048 * 16 + blockIdx.x * 16 + (wave == 0 ? 0 : 8);
+  #pragma unroll
+        for (int q = 0; q < 6; ++q) o[q] = seg_sum[q];
+      }
     }
-  }
-  if (!kPersist || p.tile_stride <= 0) break;
-  // Slot iter & 1: its next write (two tiles on) comes after the barrier
-  // that ends the next tile, when every wave has read it.
-  if (tid == 0) scratch[iter & 1] = min(p.grid + fetched, p.num_tiles);
-  __syncthreads();  // the next tile reuses the ring and the staging image
-  tile_next = __builtin_amdgcn_readfirstlane(scratch[iter & 1]);
-  if (tile_next >= p.num_tiles) break;
+    if (!kPersist || p.tile_stride <= 0) break;
+    // Slot iter & 1: its next write (two tiles on) comes after the barrier
+    // that ends the next tile, when every wave has read it.
+    if (tid == 0) scratch[iter & 1] = min(p.grid + fetched, p.num_tiles);
+    __syncthreads();  // the next tile reuses the ring and the staging image
+    tile_next = __builtin_amdgcn_readfirstlane(scratch[iter & 1]);
+    if (tile_next >= p.num_tiles) break;
   }  // tiles of a persistent workgroup
 #undef SEG_STAMP
 #undef SEG_ACCUM
