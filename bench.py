@@ -487,6 +487,9 @@ class MoeProblem:
         sp.RowIndices(self.H, self.H.row_indices)
         self.dims = (tokens, d_model, cols)
         self.flops = 2.0 * nz * d_model * 2
+        # Dense anchor: one GEMM of half the step's FLOPs (tokens x d_model
+        # x d_ff / experts, the per-expert width), reported per GEMM.
+        self.anchor_shape = (tokens, d_model, d_ff // experts)
         self.bytes = (2 * nz * 2 + tokens * d_model * 2 * 2 +
                       2 * d_model * cols * 2)
         self.dtype_code = 0 if dtype == "f16" else 1
