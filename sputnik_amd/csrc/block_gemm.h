@@ -839,34 +839,48 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         return;
       }
       // The partial (sc1, as it was stored) comes in by LDS-DMA, each
-      // wave's fragments into its own LDS region (above the scratch words),
-      // all of a half in flight at once: the accumulators leave no registers
-      // for loads, and register loads issued a few at a time cost one round
-      // trip per few KiB (8.5 us for the 256 KiB tile).
+      // wave's fragments into its own LDS region (above the scratch words):
+      // the accumulators leave no registers for loads, and register loads
+      // issued a few at a time cost one round trip per few KiB (8.5 us for
+      // the 256 KiB tile). Quarters through two buffers, so one quarter is
+      // in flight while the previous one is added.
       constexpr int kFrags = kFM * kFN;
-      constexpr int kHalfFr = kFrags / 2;
-      constexpr int kRegion = kHalfFr * 1024;
-      static_assert(16384 + kNW * kRegion <= kRingBytes && kFrags % 2 == 0,
+      constexpr int kQ = kFrags / 4;  // fragments per quarter
+      constexpr int kRegion = 2 * kQ * 1024;
+      static_assert(16384 + kNW * kRegion <= kRingBytes && kFrags % 4 == 0,
                     "pair partial staging fits in the ring");
       const __amdgpu_buffer_rsrc_t rp = pair_rsrc();
       const int lb = pair_lane_base();
       char *region = lds + 16384 + wave * kRegion;
-      const f32x4 *mine =
-          reinterpret_cast<const f32x4 *>(region) + lane;
+      auto fetch = [&](int q) {
+        char *buf = region + (q & 1) * (kQ * 1024);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+        for (int i = 0; i < kQ; ++i)
+          dma16<kSc1>(rp, buf + i * 1024, (uint32_t)(lb + (q * kQ + i) * 1024));
+      };
+      auto add = [&](int q) {
+        const f32x4 *m = reinterpret_cast<const f32x4 *>(
+                             region + (q & 1) * (kQ * 1024)) + lane;
 #pragma unroll
-        for (int i = 0; i < kHalfFr; ++i)
-          dma16<kSc1>(rp, region + i * 1024,
-                      (uint32_t)(lb + (h * kHalfFr + i) * 1024));
-        wait_vmcnt<0>();
-#pragma unroll
-        for (int i = 0; i < kHalfFr; ++i) {
-          const int f = h * kHalfFr + i;
-          acc[f / kFN][f % kFN] += mine[i * 64];
+        for (int i = 0; i < kQ; ++i) {
+          const int f = q * kQ + i;
+          acc[f / kFN][f % kFN] += m[i * 64];
         }
-        if (h == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
+        // Its buffer is refilled next: the reads must have landed.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      };
+      fetch(0);
+      fetch(1);
+      wait_vmcnt<kQ>();
+      add(0);
+      fetch(2);
+      wait_vmcnt<kQ>();
+      add(1);
+      fetch(3);
+      wait_vmcnt<kQ>();
+      add(2);
+      wait_vmcnt<0>();
+      add(3);
     }
   };
 
