@@ -1367,9 +1367,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       const int j = R - 1 - lane;
       v = lane == j ? nbr[lane] : (nbr[lane] + nbr[j] + 1) / 2;
     }
+    // Wave max by ballots, one bit at a time from the top (v < 2^16: a row
+    // holds at most 32768 blocks): SALU work, no cross-lane data movement.
+    int vmax = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d, 64));
-    pair_target = __builtin_amdgcn_readfirstlane(v);
+    for (int bit = 15; bit >= 0; --bit) {
+      const int cand = vmax | (1 << bit);
+      if (__ballot(v >= cand) != 0) vmax = cand;
+    }
+    pair_target = vmax;
     return out;
   };
   auto rank_rows = [&](int ra, int rb) {
