@@ -9,6 +9,7 @@ import ctypes
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -115,6 +116,13 @@ def summarize(buf, wgs):
                 "pipe_p50": round(float(np.median(seg["pipeline"][sel])), 2),
                 "write_p50": round(float(np.median(seg["write"][sel])), 2)}
     out["busy_us_total"] = round(float(dur.sum()), 1)
+    # In-kernel shader clock (s_memtime / s_memrealtime x 100 MHz, entry to
+    # tile written), median over workgroups (MI355X_MICROARCH.md DVFS (6)).
+    dt = (t[:, 4] - t[:, 0]).astype(np.float64)
+    dc = (t[:, 15] - t[:, 14]).astype(np.float64)
+    ok = (dt > 0) & (dc > 0)
+    if ok.any():
+        out["clock_GHz"] = round(float(np.median(dc[ok] / dt[ok] * 0.1)), 3)
     # Workgroups resident over time (10 buckets of the span).
     span = float(seg["end"].max())
     edges = np.linspace(0, span, 11)
@@ -146,8 +154,12 @@ def main():
     L.sputnik_exp_set_debug(ctypes.c_void_p(buf.data_ptr()))
     for name in names:
         keep, fn = launcher(name, device)
-        for _ in range(20):
+        warm = float(os.environ.get("TIMELINE_WARM_S", "0"))
+        t_end = time.time() + warm  # back-to-back launches so the clock settles
+        for i in range(1 << 30):
             fn()
+            if i >= 20 and (i % 50 == 0) and time.time() >= t_end:
+                break
         torch.cuda.synchronize()
         buf.zero_()
         torch.cuda.synchronize()

@@ -454,10 +454,13 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // entry, pipeline start, pipeline end, collect end, tile written, pair
   // partial published (producer), pair flag seen (consumer).
   unsigned long long tl_stamp[10] = {};
+  unsigned long long tl_cycles[2] = {};  // shader clock at stamps 0 and 4
   auto tl = [&](int i) {
     if constexpr ((SPUTNIK_EXP & 512) != 0) {
       asm volatile("" ::: "memory");
       tl_stamp[i] = __builtin_amdgcn_s_memrealtime();
+      if (i == 0) tl_cycles[0] = __builtin_amdgcn_s_memtime();
+      if (i == 4) tl_cycles[1] = __builtin_amdgcn_s_memtime();
     }
   };
   tl(0);
@@ -1738,7 +1741,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     if constexpr ((SPUTNIK_EXP & 512) != 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       tl(4);
-      if (p.debug != nullptr && wave == 0 && lane < 14) {
+      if (p.debug != nullptr && wave == 0 && lane < 16) {
         // lane i < 7 writes stamp i; then the steps, the role and the row.
         unsigned long long v = 0;
   #pragma unroll
@@ -1752,6 +1755,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         if (lane == 11) v = tl_stamp[7];
         if (lane == 12) v = tl_stamp[8];
         if (lane == 13) v = tl_stamp[9];
+      if (lane == 14) v = tl_cycles[0];
+      if (lane == 15) v = tl_cycles[1];
         p.debug[blockIdx.x * 16 + lane] = v;
       }
     }
