@@ -127,10 +127,11 @@ struct GemmParams {
   int k_limit;                 // SDD: K (elements)
   int num_tiles;               // output tiles (one-tile-per-workgroup grid)
   // Persistent launch (tall DSD / DDS, dispatch.cpp UseTall): `grid`
-  // workgroups, each running tiles blockIdx.x, + tile_stride, ... <
-  // num_tiles back to back (0: one tile per workgroup, grid = num_tiles).
+  // workgroups; workgroup b runs tile b, then the tiles it fetches from
+  // tile_counter, back to back (persistent = 0: one tile per workgroup,
+  // grid = num_tiles).
   int grid;
-  int tile_stride;
+  int persistent;
   // Persistent launches fetch their tiles past the first `grid` from this
   // counter (one atomic per tile, issued a tile ahead): tile = grid +
   // (fetched - tile_base). The host advances tile_base by num_tiles per
@@ -1420,7 +1421,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // Every branch below only sets up (srow, j0, the index segments, the step
   // range); the pipeline is then entered from ONE call site per kernel, so
   // it is inlined and the accumulators stay in registers.
-  // A persistent workgroup (p.tile_stride > 0) loops over its tiles here;
+  // A persistent workgroup (p.persistent != 0) loops over its tiles here;
   // the body still enters the pipeline from one call site.
   // (Only the non-staggered DSD / DDS configs run persistent: CfgTall.)
   constexpr bool kPersist = !Cfg::kStagger && !kSparseOut && !kSparseD;
@@ -1430,7 +1431,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     // so the atomic's round trip hides under the tile.
     int fetched = 0;
     if constexpr (kPersist) {
-      if (p.tile_stride > 0 && tid == 0)
+      if (p.persistent != 0 && tid == 0)
         fetched = (int)(atomicAdd(p.tile_counter, 1ull) - p.tile_base);
     }
     long long out_block = 0;
@@ -1523,7 +1524,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       }
     } else {
       // ==== one output tile per workgroup ===================================
-      const int tile = kPersist && p.tile_stride > 0 ? tile_next
+      const int tile = kPersist && p.persistent != 0 ? tile_next
                        : (SPUTNIK_EXP & 8) ? (int)blockIdx.x
                                            : xcd_tile(blockIdx.x, gridDim.x);
       if constexpr (kGroupedSdd) {
@@ -1768,7 +1769,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         for (int q = 0; q < 6; ++q) o[q] = seg_sum[q];
       }
     }
-    if (!kPersist || p.tile_stride <= 0) break;
+    if (!kPersist || p.persistent == 0) break;
     // Slot iter & 1: its next write (two tiles on) comes after the barrier
     // that ends the next tile, when every wave has read it.
     if (tid == 0) scratch[iter & 1] = min(p.grid + fetched, p.num_tiles);

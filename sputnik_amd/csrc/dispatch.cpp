@@ -588,7 +588,7 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
     slot->base = 0;
   }
   p->grid = slots;
-  p->tile_stride = slots;
+  p->persistent = 1;
   p->tile_counter = slot->counter;
   p->tile_base = slot->base;
   slot->base += (unsigned long long)p->num_tiles;  // this launch's fetches
