@@ -361,3 +361,33 @@ def test_graph_capture_with_pairs():
         sp.MatmulEx(A.m, False, Bd.m, False, C)
         _equal(got, want, "eager between replays")
     assert sp.pair_errors() == 0
+
+
+def test_graph_capture_tall_persistent():
+    """A tall DSD captured into a graph on a stream whose persistent tile
+    counter already exists: the captured launch runs one tile per workgroup
+    (the counter base is host state), so replays interleaved with eager
+    persistent launches on the same stream all stay exact."""
+    rng = np.random.default_rng(12)
+    A = ISparse(65536, 256, 0.3, rng, "f16")
+    Bd = IDense(256, 512, rng, "f16")
+    want = _expect(A.dense.astype(np.float64) @ Bd.values, "f16")
+    C, got = _nan_out(65536, 512, "f16")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        sp.MatmulEx(A.m, False, Bd.m, False, C)  # creates s's counter
+    torch.cuda.current_stream().wait_stream(s)
+    _equal(got, want, "eager on s")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+    for _ in range(3):
+        got.fill_(float("nan"))
+        g.replay()
+        _equal(got, want, "graph replay")
+        got.fill_(float("nan"))
+        with torch.cuda.stream(s):
+            sp.MatmulEx(A.m, False, Bd.m, False, C)
+        s.synchronize()
+        _equal(got, want, "eager persistent between replays")
