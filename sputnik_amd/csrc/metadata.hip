@@ -152,6 +152,12 @@ __global__ void __launch_bounds__(kTransposeThreads)
   // 2. Per-column word prefix counts (one wave per column, 64 words a pass)
   //    and column totals.
   const int wave = tid >> 6;
+  if (words == 1) {  // <= 32 block-rows: one word per column, no scan
+    for (int cl = tid; cl < ncols; cl += kTransposeThreads) {
+      prefix[cl] = 0;
+      partial[cl] = __popc(bits[cl]);
+    }
+  } else
   for (int cl = wave; cl < ncols; cl += kTransposeWaves) {
     int run = 0;
     for (int w0 = 0; w0 < words; w0 += 64) {
@@ -172,14 +178,32 @@ __global__ void __launch_bounds__(kTransposeThreads)
 
   // 3. Exclusive scan of the column totals -> offsets_t (slice <= threads:
   //    thread t owns column c0 + t).
-  const int mine = tid < ncols ? partial[tid] : 0;
-  int unused;
-  const int first = base + block_exclusive_scan(mine, wsum, &unused);
-  if (tid < ncols) {
-    partial[tid] = first;  // first slot of column c0 + tid
-    offsets_t[c0 + tid] = first;
+  if (ncols <= 64) {  // one wave scans (no workgroup scan barriers)
+    if (wave == 0) {
+      const int v = lane < ncols ? partial[lane] : 0;
+      int incl = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += t;
+      }
+      const int first = base + incl - v;
+      if (lane < ncols) {
+        partial[lane] = first;  // first slot of column c0 + lane
+        offsets_t[c0 + lane] = first;
+      }
+      if (c1 == block_cols && lane == 0) offsets_t[block_cols] = blocks;
+    }
+  } else {
+    const int mine = tid < ncols ? partial[tid] : 0;
+    int unused;
+    const int first = base + block_exclusive_scan(mine, wsum, &unused);
+    if (tid < ncols) {
+      partial[tid] = first;  // first slot of column c0 + tid
+      offsets_t[c0 + tid] = first;
+    }
+    if (c1 == block_cols && tid == 0) offsets_t[block_cols] = blocks;
   }
-  if (c1 == block_cols && tid == 0) offsets_t[block_cols] = blocks;
   __syncthreads();
 
   // 4. Scatter: slot = column start + rank of the block-row in its column.
