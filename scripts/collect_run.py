@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Copy one scripts/gpu_measure.sh run from gpurun_out/TAG into the tracked
+profiles/r02/TAG: each step's JSON line, the rocprofv3 kernel stats of the
+headline, the step log, and the junit summary (profiles/r02_gputest_summary.json).
+Usage: scripts/collect_run.py TAG"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles", "r02", tag)
+    os.makedirs(dst, exist_ok=True)
+    for f in sorted(os.listdir(src)):
+        if not f.endswith(".log") or f in ("smoke.log", "pytest_gpu.log",
+                                           "prof.log", "steps.log"):
+            continue
+        last = [l for l in open(os.path.join(src, f)) if l.startswith("{")]
+        if last:
+            json.loads(last[-1])
+            open(os.path.join(dst, f[:-4] + ".json"), "w").write(last[-1])
+    shutil.copy(os.path.join(src, "steps.log"), dst)
+    ks = os.path.join(src, "prof", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, "dsd4096_d50_kernel_stats.csv"))
+    junit = os.path.join(src, "junit.xml")
+    if os.path.exists(junit):
+        subprocess.check_call([sys.executable,
+                               os.path.join(ROOT, "scripts", "junit_summary.py"),
+                               junit,
+                               os.path.join(ROOT, "profiles",
+                                            "r02_gputest_summary.json"), tag])
+    print("collected", tag, "->", dst)
+
+
+if __name__ == "__main__":
+    main()
