@@ -84,6 +84,10 @@
 #define SPUTNIK_SDD_BLOCK_LOOP 1
 #endif
 // Staggered configs: static s_setprio(1) for the lagging (younger) half.
+// Tall configuration: scalar index loads (see kScalarIdx).
+#ifndef SPUTNIK_TALL_SIDX
+#define SPUTNIK_TALL_SIDX 1
+#endif
 #ifndef SPUTNIK_LAG_PRIO
 #define SPUTNIK_LAG_PRIO 1
 #endif
@@ -406,8 +410,13 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr int kRingBytes = kStages * kStageBytes;
   // Index list staged per chunk in LDS (smaller when three workgroups share
   // a CU); staggered configs read it with scalar loads instead.
+  // The tall configuration (CfgTall, persistent, 0-3 blocks per tile at
+  // config 5) reads it with scalar loads too: no staging round trip and no
+  // barrier pair per tile (SPUTNIK_TALL_SIDX=0: staged).
+  constexpr bool kTallCfg = std::is_same<Cfg, CfgTall>::value && !kSparseOut;
   constexpr bool kScalarIdx =
-      Cfg::kStagger && !kSparseIn && !kSparseD;
+      (Cfg::kStagger || (SPUTNIK_TALL_SIDX != 0 && kTallCfg)) && !kSparseIn &&
+      !kSparseD;
   constexpr int kIndexChunk = Cfg::kWGs >= 3 ? 256 : kMaxIndexChunk;
   constexpr bool kDenseS = kSparseOut && !kSparseIn;  // SDD
   static_assert(!kSparseIn || (kSparseOut &&
@@ -423,7 +432,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr int kDssMaxK = 256;  // k-blocks (K <= 32768, as the reference)
   constexpr int kIdxBytes =
       kDenseS ? (Cfg::kStagger ? 0 : 16)
-                 : (kScalarIdx ? 0 : kIndexChunk * 6 + 16);
+              : (kScalarIdx ? (Cfg::kStagger ? 0 : 16) : kIndexChunk * 6 + 16);
   // SDD with kBN > 128: a tile is a group of up to kGrp stored blocks of one
   // block-row, found in-kernel from C's offsets (rows <= kMaxGroupRows).
   constexpr bool kGroupedSdd = kDenseS && kBN > kBlock;
@@ -772,7 +781,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // stored and loaded sc1 (L1 bypass, write-through), each storing wave
   // drains vmcnt before a barrier, then ONE lane stores the flag (relaxed,
   // agent scope = sc1) and the consumer polls it with sc1 loads.
-  constexpr bool kPairs = kScalarIdx && !kSparseOut;
+  constexpr bool kPairs = kScalarIdx && !kSparseOut && Cfg::kStagger;
   constexpr int kSlotBytes = kBM * kBN * 4;
   constexpr int kSc1 = 16;  // cache-policy bits: sc1
   int pair_id = 0;
@@ -1691,6 +1700,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
             entries = __builtin_amdgcn_readfirstlane(offs[srow + 1]) - entry0;
             __syncthreads();  // staged offsets / scratch read by every wave
           }
+        } else if constexpr (kScalarIdx) {
+          entry0 = scalar_load_int(p.s_offsets, srow);
+          entries = scalar_load_int(p.s_offsets, srow + 1) - entry0;
         } else {
           entry0 = p.s_offsets[srow];
           entries = p.s_offsets[srow + 1] - entry0;
