@@ -23,12 +23,26 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
-    ap.add_argument("--op", default="dsd", choices=["dsd", "sdd", "moe_sdd", "moe_dsd"])
+    ap.add_argument("--op", default="dsd",
+                    choices=["dsd", "sdd", "moe_sdd", "moe_dsd", "pair", "moe"])
     args = ap.parse_args()
     import torch
     import bench
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    if args.op in ("pair", "moe"):
+        # Whole BASELINE workloads (config 3 / config 4) through bench.py's
+        # own launchers, one per variant library.
+        import sputnik_amd as sp
+        prob = (bench.PairProblem(args.k, args.density, args.dtype, 0, dev)
+                if args.op == "pair" else bench.MoeProblem("bf16", 0, dev))
+        fns = []
+        for path in args.libs:
+            sp._lib = None
+            sp.LIB_PATH = os.path.abspath(path)
+            launch = prob.launcher()
+            fns.append((os.path.basename(path), lambda f=launch: f(), ()))
+        return report(args, prob, fns)
     if args.op == "dsd":
         import numpy as np
         from sputnik_amd import matrix_utils as mu
@@ -72,6 +86,11 @@ def main():
              prob.dtype_code, stream)
         assert fn(*a) == 0, path
         fns.append((os.path.basename(path), fn, a))
+    return report(args, prob, fns)
+
+
+def report(args, prob, fns):
+    import torch
     times = {n: [] for n, _, _ in fns}
     for _ in range(3):
         for n, fn, a in fns:
