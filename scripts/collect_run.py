@@ -29,6 +29,14 @@ def main():
     ks = os.path.join(src, "prof", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "dsd4096_d50_kernel_stats.csv"))
+    for w in ("sdd_dds", "panel"):
+        ks = os.path.join(src, "prof_" + w, "run_kernel_stats.csv")
+        if os.path.exists(ks):
+            shutil.copy(ks, os.path.join(dst, w + "_kernel_stats.csv"))
+    pmc = os.path.join(src, "pmc_latest.json")
+    if os.path.exists(pmc):
+        shutil.copy(pmc, os.path.join(dst, "pmc_latest.json"))
+        shutil.copy(pmc, os.path.join(ROOT, "profiles", "pmc_latest.json"))
     junit = os.path.join(src, "junit.xml")
     if os.path.exists(junit):
         subprocess.check_call([sys.executable,

@@ -37,6 +37,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run --
   python3 $R/bench.py --sweep "" --no-cpu > $OUT/prof.log 2>&1; rc=$?
 echo "== prof rc=$rc" | tee -a $OUT/steps.log; tail -2 $OUT/prof.log
 fatal $rc && exit $rc
+for w in sdd_dds panel; do
+  echo "== prof_$w" | tee -a $OUT/steps.log
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof_$w -o run -- \
+    python3 $R/bench.py --workload $w > $OUT/prof_$w.log 2>&1; rc=$?
+  echo "== prof_$w rc=$rc" | tee -a $OUT/steps.log
+  fatal $rc && exit $rc
+done
 cd $R
 for w in sdd_dds moe panel transpose; do
   step w_$w 300 python bench.py --workload $w; rc=$?; fatal $rc && exit $rc
