@@ -147,12 +147,14 @@ struct GemmParams {
   // grid = num_tiles).
   int grid;
   int persistent;
-  // Persistent launches fetch their tiles past the first `grid` from this
-  // counter (one atomic per tile, issued a tile ahead): tile = grid +
-  // (fetched - tile_base). The host advances tile_base by num_tiles per
-  // launch, exactly the launch's fetches, so the counter is never reset.
+  // Persistent launches fetch their tiles past the first `grid` from
+  // tile_counter[0] (one atomic per tile, issued a tile ahead): tile = grid +
+  // fetched. Each launch starts from zero and leaves zero behind: a
+  // workgroup whose fetch ran past the last tile arrives on tile_counter[1],
+  // and the grid's last arriver resets both words. No host-side state
+  // advances per launch, so launch order, a failed launch or a second host
+  // thread on the stream cannot skew the tile numbering.
   unsigned long long *tile_counter;
-  unsigned long long tile_base;
   // Pair balancing (staggered one-workgroup-per-CU configs, see the
   // kernel): the block-rows of each panel are paired heaviest-with-lightest;
   // the light workgroup also computes the head of the heavy row and hands it
@@ -164,6 +166,11 @@ struct GemmParams {
   unsigned pair_epoch;         // this launch's epoch (never 0)
   unsigned *pair_error;        // set to 1 when a consumer timed out
   int pair_fault;              // test knob: producers never publish
+  // Pair launches with 8 panels: XCD x (= workgroup b mod 8) takes panels
+  // 2(x/2) and 2(x/2)+1 for half of the pairs instead of one panel for all
+  // of them, so it streams half of S (each block used by two tiles) and
+  // two D panels (host: dispatch.cpp PreparePairs).
+  int pair_xcd2;
   unsigned long long *debug;   // SPUTNIK_EXP & 128 builds only
   // DSS (dense = sparse x sparse): op(B)'s column lists (k-block, storage
   // block) — B's transposed metadata, or its own when op(B) = B^T.
@@ -1459,7 +1466,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     int fetched = 0;
     if constexpr (kPersist) {
       if (p.persistent != 0 && tid == 0)
-        fetched = (int)(atomicAdd(p.tile_counter, 1ull) - p.tile_base);
+        fetched = (int)atomicAdd(p.tile_counter, 1ull);
     }
     long long out_block = 0;
     int entry0 = 0, entries = 0;   // sparse S: the row's CSR entry range
@@ -1488,20 +1495,34 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       const int n_solo = p.num_jtiles * (R & 1);
       const int bid = blockIdx.x;
       int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
+      // GemmParams::pair_xcd2 (8 panels, no middle row, an even number of
+      // pairs): XCD x = b mod 8 takes panels 2(x/2), 2(x/2)+1 and pairs
+      // [(x mod 2) half/2, +half/2). A bijection on each role's (panel,
+      // pair), so producers still precede their consumers.
+      // (DSD only: measured there.)
+      const bool xcd2 = !kOutT && p.pair_xcd2 != 0 && p.num_jtiles == 8 &&
+                        n_solo == 0 && (half & 1) == 0;
+      auto place = [&](int b) {
+        if (xcd2) {
+          const int x = b & 7, k = b >> 3;
+          panel = 2 * (x >> 1) + (k & 1);
+          pi = (x & 1) * (half >> 1) + (k >> 1);
+        } else {
+          const int t = xcd_tile(b, n_light);
+          panel = t / half;
+          pi = t % half;
+        }
+      };
       if (bid < n_light) {
         role = 0;
-        const int t = xcd_tile(bid, n_light);
-        panel = t / half;
-        pi = t % half;
+        place(bid);
       } else if (bid < n_light + n_solo) {
         role = 1;
         panel = bid - n_light;
         pi = half;
       } else {
         role = 2;
-        const int t = xcd_tile(bid - n_light - n_solo, n_light);
-        panel = t / half;
-        pi = t % half;
+        place(bid - n_light - n_solo);
       }
       int2 rows;
       int e_h, n_h, e_l, n_l;
@@ -1805,7 +1826,20 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     if (tid == 0) scratch[iter & 1] = min(p.grid + fetched, p.num_tiles);
     __syncthreads();  // the next tile reuses the ring and the staging image
     tile_next = __builtin_amdgcn_readfirstlane(scratch[iter & 1]);
-    if (tile_next >= p.num_tiles) break;
+    if (tile_next >= p.num_tiles) {
+      // This workgroup makes no further fetch: arrive; the last arriver
+      // (every fetch of the launch is then done) resets the counter pair.
+      if (tid == 0) {
+        const unsigned long long d = atomicAdd(p.tile_counter + 1, 1ull);
+        if (d + 1 == (unsigned long long)p.grid) {
+          __hip_atomic_store(p.tile_counter, 0ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.tile_counter + 1, 0ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      break;
+    }
   }  // tiles of a persistent workgroup
 #undef SEG_STAMP
 #undef SEG_ACCUM

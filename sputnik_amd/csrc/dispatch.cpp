@@ -73,16 +73,31 @@ static PairSlot g_pairs[kMaxPairSlots];
 static std::mutex g_pairs_mu;
 static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
 
-// Tile counter of persistent tall launches, per (device, stream): each
-// launch makes exactly num_tiles fetches, so the host advances `base` and the
-// counter is never reset (stream order; not used under graph capture).
+// Tile counter pair of persistent tall launches, per (device, stream): the
+// kernel resets it to zero at the end of every launch (GemmParams::
+// tile_counter), so launches on one stream need no host-side bookkeeping.
+// Not used under graph capture (a replay on another stream could overlap an
+// eager launch on this one) nor on hipStreamPerThread, whose one handle
+// stands for many concurrently running streams.
 struct CounterSlot {
   int device = -1;
   hipStream_t stream = nullptr;
-  unsigned long long *counter = nullptr;
-  unsigned long long base = 0;
+  unsigned long long *counter = nullptr;  // [fetch, done]
 };
 static CounterSlot g_counters[kMaxPairSlots];
+
+// A (device, stream) table ran out of slots: the caller falls back to the
+// plain launch (correct, slower); said once per process.
+static void WarnSlotsFull(const char *what) {
+  static bool warned[2] = {false, false};
+  const int i = what[0] == 'p' ? 0 : 1;
+  if (!warned[i]) {
+    warned[i] = true;
+    SPUTNIK_LOG(WARNING) << "sputnik-amd: more than " << kMaxPairSlots
+                         << " streams use " << what
+                         << "; further streams run without it";
+  }
+}
 
 static bool PairsEnabled() {
 #ifdef SPUTNIK_NO_PAIRS
@@ -104,12 +119,16 @@ static bool PairsEnabled() {
 #ifndef SPUTNIK_PAIR_MIN_MEAN4
 #define SPUTNIK_PAIR_MIN_MEAN4 8  // 4 x mean blocks per row
 #endif
+#ifndef SPUTNIK_PAIR_XCD2_DEFAULT
+#define SPUTNIK_PAIR_XCD2_DEFAULT 1
+#endif
 static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair = 0;
   if (!CfgSparse::kStagger || CfgSparse::kWGs != 1)
     return;
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
+  if (stream == hipStreamPerThread) return;  // many streams, one handle
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
       cs != hipStreamCaptureStatusNone)
@@ -129,7 +148,10 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
         slot = &s;
         break;
       }
-    if (slot == nullptr) return;
+    if (slot == nullptr) {
+      WarnSlotsFull("pair balancing");
+      return;
+    }
     const int cus = DeviceCUs(dev);
     if (cus <= 0) return;
     const int slots = cus * CfgSparse::kWGs;
@@ -161,21 +183,30 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair_epoch = slot->epoch;
   p->pair_error = slot->flags + slot->pairs;
   p->pair_fault = g_pair_fault;
+  // Two panels x half the pairs per XCD (GemmParams::pair_xcd2) from a mean
+  // of 8 blocks per row: DSD 4096^3 A/B (r02m) 30% / 50% / 90% +1.2 / +2.7
+  // / +2.8%, 10% -4.4%. SPUTNIK_AMD_PAIR_XCD2=0 turns it off.
+  static const int xcd2 = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_PAIR_XCD2");
+    return e != nullptr ? std::atoi(e) : SPUTNIK_PAIR_XCD2_DEFAULT;
+  }();
+  p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? 1 : 0;
 }
 
 // Pair hand-offs that timed out since the last call, over every workspace of
-// the current device (synchronizes each workspace's stream); the error words
-// are cleared.
+// the current device; the error words are cleared. One device-wide
+// synchronize first: the streams the workspaces were made for may have been
+// destroyed since (or their handles reused), so they are never used here.
 int PairErrors() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
   int total = 0;
   for (auto &s : g_pairs) {
     if (s.partials == nullptr || s.device != dev) continue;
     unsigned word = 0;
-    if (hipStreamSynchronize(s.stream) != hipSuccess ||
-        hipMemcpy(&word, s.flags + s.pairs, sizeof(word),
+    if (hipMemcpy(&word, s.flags + s.pairs, sizeof(word),
                   hipMemcpyDeviceToHost) != hipSuccess)
       return -1;
     if (word != 0) {
@@ -558,6 +589,7 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   const int cus = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
   const int slots = cus * CfgTall::kWGs;
   if (!persistent || slots <= 0 || p->num_tiles <= slots) return true;
+  if (stream == hipStreamPerThread) return true;  // many streams, one handle
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
       cs != hipStreamCaptureStatusNone)
@@ -575,23 +607,23 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
         slot = &c;
         break;
       }
-    if (slot == nullptr) return true;
+    if (slot == nullptr) {
+      WarnSlotsFull("persistent launches");
+      return true;
+    }
     unsigned long long *ctr = nullptr;
-    if (hipMalloc(&ctr, sizeof(*ctr)) != hipSuccess) return true;
-    if (hipMemset(ctr, 0, sizeof(*ctr)) != hipSuccess) {
+    if (hipMalloc(&ctr, 2 * sizeof(*ctr)) != hipSuccess) return true;
+    if (hipMemset(ctr, 0, 2 * sizeof(*ctr)) != hipSuccess) {
       (void)hipFree(ctr);
       return true;
     }
     slot->device = dev;
     slot->stream = stream;
     slot->counter = ctr;
-    slot->base = 0;
   }
   p->grid = slots;
   p->persistent = 1;
   p->tile_counter = slot->counter;
-  p->tile_base = slot->base;
-  slot->base += (unsigned long long)p->num_tiles;  // this launch's fetches
   return true;
 }
 
