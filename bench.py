@@ -13,11 +13,13 @@ benchmark (dsd_benchmark.cu:82-107): 50 ms idle, W warm-up calls, K timed
 calls between HIP events on the launch stream; barrier + synchronize on both
 sides; max over ranks.
 
-Multi-GPU (`--gpus N`, launched by torch.distributed.run): one BCSR matrix of
-N x 4096 rows (the same topology on every rank, from a shared seed) is split
-with the library's own
-shard_rows_by_nnz / slice_block_rows; every rank runs its row
-panel against a replicated B; no collective on the hot path. Weak scaling:
+Multi-GPU (`--gpus N`, launched by torch.distributed.run): one BCSR matrix
+(the same topology on every rank, from a shared seed) is split with the
+library's own shard_rows_by_nnz / slice_block_rows; every rank
+runs its row panel against a replicated B; no collective on the hot path.
+`--scaling strong` (the default): the matrix is the metric's own M=K=N=4096,
+so N ranks share its 32 block-rows (BASELINE metric "DSD M=K=N=4096 @
+1/2/4/8 GPU"). `--scaling weak`: N x 4096 rows, 4096 per rank. Either way
 value = nnz-FLOPs of all ranks / max-rank time.
 
 Other workloads (`--workload`): sdd_dds (config 3), moe (config 4), panel
@@ -71,7 +73,11 @@ def parse():
     ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"])
     ap.add_argument("--trans", default="NN", choices=["NN", "NT", "TN", "TT"])
     ap.add_argument("--api", default="ex", choices=["ex", "matmul"])
-    ap.add_argument("--m", type=int, default=4096, help="rows per rank")
+    ap.add_argument("--m", type=int, default=4096,
+                    help="rows of the DSD matrix (strong) or per rank (weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: ranks split one M-row matrix (the metric's "
+                         "4096^3); weak: N x M rows, M per rank")
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--density", type=float, default=0.5)
@@ -746,14 +752,15 @@ def main():
                                   if d and float(d) != args.density]
     results = {}
     head = None
+    m_total = args.m if args.scaling == "strong" else args.m * world
     for d in densities:
-        prob = dsd_panel(args, world, rank, device, d)
+        prob = dsd_panel(args, world, rank, device, d, m_total=m_total)
         fn = prob.launcher()
         ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
         per_step = ms / args.steps
         flops_all = sum_over_ranks(prob.flops, world)
         tflops = flops_all / (per_step * 1e-3) / 1e12
-        key = f"dsd_{prob.m}x{args.k}x{args.n}_{d}_{args.dtype}"
+        key = f"dsd_{m_total}x{args.k}x{args.n}_{d}_{args.dtype}"
         traffic, note = pmc_traffic(args.pmc, key, build.get("hash"))
         roof = roofline(prob.flops, prob.bytes, per_step * 1e-3, prob.kernel,
                         traffic)
@@ -773,7 +780,7 @@ def main():
     anchor = None
     if rank == 0:
         kd = max(BLOCK, int(round(args.k * args.density / BLOCK)) * BLOCK)
-        anchor = dense_anchor(args.m, args.n, kd, args.dtype, device)
+        anchor = dense_anchor(prob.m, args.n, kd, args.dtype, device)
         if "tflops" in anchor:
             anchor["sparse_over_dense"] = round(tflops / world / anchor["tflops"], 3)
 
@@ -794,20 +801,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(per_step, 5),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (RANDOM_UNIFORM block topology, U(-1,1) values)",
             "config": {
-                "workload": f"DSD block=128 M={args.m}/rank K={args.k} "
+                "workload": f"DSD block=128 M={m_total} K={args.k} "
                             f"N={args.n} density={args.density} "
                             f"{args.dtype} (NN, MatmulEx)",
-                "block": 128, "m_per_rank": args.m, "k": args.k, "n": args.n,
+                "block": 128, "m": m_total, "k": args.k, "n": args.n,
                 "density": args.density,
-                "parallelism": (f"row panels of one {args.m * world}-row "
+                "parallelism": (f"row panels of one {m_total}-row "
                                 f"matrix split by nnz over {world} rank(s) "
                                 f"(rank 0: block-rows {r0}..{r1 - 1}), "
-                                "no collective"),
+                                f"no collective ({args.scaling} scaling)"),
             },
             "by_density": {str(k): v for k, v in results.items()},
             "roofline": roof,

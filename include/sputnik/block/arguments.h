@@ -73,7 +73,10 @@ inline BlockSize AsBlockSize(int b) {
 //                           storage index per block in column order).
 //   row_indices           — int16[#blocks], block-row of each stored block
 //                           (sparse outputs).
-//   bitmask               — sparse x sparse products (not implemented here).
+//   bitmask               — uint64 bit matrix of the block pattern, filled by
+//                           Bitmask() (block/bitmask/bitmask.h); DSS does not
+//                           need it here (it intersects rows and columns in
+//                           LDS) but reference DSS callers allocate it.
 //   create_metadata       — Matmul builds the transposed metadata when true;
 //                           MatmulEx clears it so precomputed metadata is used.
 struct BlockMatrix {

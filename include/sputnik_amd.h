@@ -155,15 +155,17 @@ const char *sputnik_version(void);
 const char *sputnik_build_hash(void);
 
 /* ---- Diagnostics (need a device) */
-/* SDD tile plan: 1 = grouped 128x512 tiles (>= 6 blocks per CU), 0 = one
+/* SDD tile plan: 1 = grouped 128x512 tiles (>= 5 blocks per CU), 0 = one
  * k-split 128x128 block per workgroup, -1 = the problem is rejected. */
 int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_block_matrix_t *c);
-/* Number of pair-balancing workspaces of the current device in which a
- * consumer workgroup timed out waiting for its partial since the last call
- * (its output tile was written as NaN); clears them. Synchronizes. -1 on a
- * HIP error. */
+/* Number of pair hand-offs on the current device whose consumer workgroup
+ * timed out waiting for its partial (a bounded 0.2 s wait) since the last
+ * call; such a consumer's output tile is written as NaN, never as a partial
+ * sum. Callers that share the GPU with other work can poll this after a
+ * launch to detect the (otherwise unobserved) event. Clears the counts.
+ * Synchronizes the device. -1 on a HIP error. */
 int sputnik_pair_errors(void);
 /* Test knob: when on, pair producers never publish (forces the timeout). */
 void sputnik_debug_pair_fault(int on);

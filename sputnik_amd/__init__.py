@@ -359,7 +359,8 @@ def sdd_plan(a, transpose_a, b, transpose_b, c) -> int:
 
 
 def pair_errors() -> int:
-    """Timed-out pair hand-offs since the last call (their tiles are NaN)."""
+    """Pair hand-offs since the last call whose consumer timed out (its
+    output tile is NaN; sputnik_pair_errors() in include/sputnik_amd.h)."""
     return int(lib().sputnik_pair_errors())
 
 

@@ -164,13 +164,21 @@ struct GemmParams {
   unsigned *pair_flags;        // #pairs; holds the epoch of the launch whose
                                // producer published last (never reset)
   unsigned pair_epoch;         // this launch's epoch (never 0)
-  unsigned *pair_error;        // set to 1 when a consumer timed out
+  unsigned *pair_error;        // += 1 per consumer that timed out
   int pair_fault;              // test knob: producers never publish
   // Pair launches with 8 panels: XCD x (= workgroup b mod 8) takes panels
   // 2(x/2) and 2(x/2)+1 for half of the pairs instead of one panel for all
   // of them, so it streams half of S (each block used by two tiles) and
   // two D panels (host: dispatch.cpp PreparePairs).
   int pair_xcd2;
+  // Split mode (pair_split = 2; at most half as many tiles as CUs, e.g. the
+  // 512 to 2048-row panels of a strong-scaled 4096^2): grid = 2 x
+  // num_tiles. The tile's row is cut into two halves of its blocks; the
+  // first half's workgroup (dispatched first) publishes its fp32 partial,
+  // the second half's adds it and writes the tile. (4 and 8 chunks were
+  // slower at every panel height measured: each further partial costs its
+  // consumer a 256 KiB collect, r03b.)
+  int pair_split;
   unsigned long long *debug;   // SPUTNIK_EXP & 128 builds only
   // DSS (dense = sparse x sparse): op(B)'s column lists (k-block, storage
   // block) — B's transposed metadata, or its own when op(B) = B^T.
@@ -302,10 +310,15 @@ __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
 // sets the register budget through __launch_bounds__ and must match the LDS
 // footprint).
 template <int BN_, int WM_, int WN_, int BK_, int STAGES_, int WGS_,
-          int STAGGER_ = 0, int KSPLIT_ = 1>
+          int STAGGER_ = 0, int KSPLIT_ = 1, int SPLITMODE_ = 0>
 struct TileConfig {
   static constexpr int kBN = BN_, kWM = WM_, kWN = WN_, kBK = BK_;
   static constexpr int kStages = STAGES_, kWGs = WGS_;
+  // The pair split mode (GemmParams::pair_split) is its own instantiation,
+  // so the pair-balanced kernel's register allocation is not disturbed by it
+  // (with both in one kernel, hipcc spills an accumulator in the last
+  // block's steps).
+  static constexpr bool kSplitMode = SPLITMODE_ != 0;
   // kKSplit = 2: two wave sets own the same kWM x kWN sub-tiles and split
   // each slot's k depth between them (set h takes k-half h); their fp32
   // accumulators are summed through LDS before the epilogue.
@@ -336,6 +349,8 @@ using CfgWide8 = TileConfig<512, 2, 4, 32, 3, 1>;
 // (the whole 160 KiB LDS; the sparse index list is then read with scalar
 // loads, not staged), pair-balanced across block-rows (dispatch.cpp).
 using CfgWide8S = TileConfig<512, 2, 4, 32, 4, 1, 1>;
+// The same tile in split mode: two workgroups per tile (few tiles).
+using CfgWide8Split = TileConfig<512, 2, 4, 32, 4, 1, 1, 1, 1>;
 // SDD: one 128x128 output block per workgroup, 4 waves of 64x64, BK=64.
 using CfgBlock = TileConfig<128, 2, 2, 64, 3, 1>;
 // SDD, one block per workgroup with K split inside it: 8 waves in two
@@ -356,6 +371,7 @@ using CfgBlock2 = TileConfig<128, 2, 2, 32, 3, 2>;
 #define SPUTNIK_SPARSE_CFG CfgWide8S
 #endif
 using CfgSparse = SPUTNIK_SPARSE_CFG;  // DSD / DDS tile configuration
+using CfgSplit = CfgWide8Split;        // DSD / DDS in split mode
 // DSD / DDS over tall sparse operands (more block-rows than kLptRows).
 #ifndef SPUTNIK_TALL_CFG
 #define SPUTNIK_TALL_CFG CfgDual
@@ -380,14 +396,19 @@ using CfgSs = SPUTNIK_SS_CFG;          // SSD / SDS tile configuration
 #endif
 using CfgDss = SPUTNIK_DSS_CFG;        // DSS tile configuration
 
-// Bounded spin for the pair hand-off (about 0.1 s): a launch can never hang
-// on a missing partial. The producer never waits and always has a lower
-// workgroup index than its consumer (in-order dispatch), so the bound is a
-// guard, not part of the protocol. A consumer that gives up does not use the
-// partial: it poisons its tile with NaN and raises GemmParams::pair_error
-// (read by sputnik_pair_errors()), and the per-launch epoch keeps a late
-// publish from satisfying any later launch.
-constexpr int kSpinLimit = 1 << 22;
+// Bounded wait for the pair hand-off: a launch can never hang on a missing
+// partial. The producer never waits and always has a lower workgroup index
+// than its consumer (in-order dispatch), so the bound is a guard, not part
+// of the protocol: 0.2 s (s_memrealtime, 100 MHz), ~3000x the longest tile
+// at 4096^2 x 4096, long enough to ride out a time-sliced preemption of the
+// producer. A consumer that gives up does not use the partial: it poisons
+// its tile with NaN (never a silently wrong number) and counts the event in
+// GemmParams::pair_error (sputnik_pair_errors()); the per-launch epoch keeps
+// a late publish from satisfying any later launch. (A consumer that instead
+// recomputes the head itself was built three ways in r03 — a second pass of
+// the pipeline, a cold in-kernel path, a non-inlined function — and every
+// one pushed the kernel's hot path into scratch, 2-4 us per tile.)
+constexpr unsigned long long kPairWaitTicks = 20000000;
 
 // kSparseOut: sparse output block. With kSparseIn = false that is SDD (dense
 // S); with kSparseIn = true, SSD / SDS (sparse S, as DSD / DDS, restricted to
@@ -836,25 +857,23 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   };
   // Consumer side: poll for this launch's epoch, barrier, add the partial
   // (sc1 loads). The flag is never reset: a publish from an earlier launch
-  // carries an older epoch, so it can never satisfy this one. On timeout the
-  // partial is not used: the tile becomes NaN and the error word is raised.
-  auto collect = [&]() {
+  // carries an older epoch, so it can never satisfy this one. Returns false
+  // on timeout: the tile is NaN and the event counted in the error word.
+  auto collect = [&]() -> bool {
     if constexpr (kPairs) {
       int *ok = scratch + 3;
       if (tid == 0) {
-        int spins = 0;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         bool got;
         while (!(got = __hip_atomic_load(p.pair_flags + pair_id,
                                          __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) ==
                        p.pair_epoch) &&
-               spins < kSpinLimit) {
+               __builtin_amdgcn_s_memrealtime() - t0 < kPairWaitTicks)
           __builtin_amdgcn_s_sleep(1);
-          ++spins;
-        }
         if (!got)
-          __hip_atomic_store(p.pair_error, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_add(p.pair_error, 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         *ok = got ? 1 : 0;
       }
       wait_vmcnt<0>();  // no DMA of the pipeline still lands in the ring
@@ -867,7 +886,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         for (int a = 0; a < kFM; ++a)
 #pragma unroll
           for (int b = 0; b < kFN; ++b) acc[a][b] = f32x4{nan, nan, nan, nan};
-        return;
+        return false;
       }
       // The partial (sc1, as it was stored) comes in by LDS-DMA, each
       // wave's fragments into its own LDS region (above the scratch words):
@@ -913,6 +932,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       wait_vmcnt<0>();
       add(3);
     }
+    return true;
   };
 
   // flush_at > 0: after the MFMAs of step flush_at - 1 the accumulators are
@@ -1459,6 +1479,11 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // the body still enters the pipeline from one call site.
   // (Only the non-staggered DSD / DDS configs run persistent: CfgTall.)
   constexpr bool kPersist = !Cfg::kStagger && !kSparseOut && !kSparseD;
+  // Split mode: the first num_tiles workgroups only publish partials
+  // (recomputed from the launch, not kept live across the pipeline).
+  auto split_producer = [&]() {
+    return kPairs && Cfg::kSplitMode && (int)blockIdx.x < p.num_tiles;
+  };
   int tile_next = blockIdx.x;
   for (int iter = 0;; ++iter) {
     // The tile after this one: fetched now, used after this tile's epilogue,
@@ -1476,7 +1501,29 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     bool use_pairs = false;
     if constexpr (kPairs) use_pairs = p.pair != 0;
     tl(7);
-    if (use_pairs) {
+    if (Cfg::kSplitMode) {
+      // ==== split mode: two workgroups per tile (GemmParams::pair_split) ===
+      // Chunk g of the tile's row is entries [g n / 2, (g+1) n / 2). Grid
+      // order [chunk 0 x T] [chunk 1 x T]: every producer precedes its
+      // consumer in dispatch order, as in the pair mode below.
+      const int nt = p.num_tiles;
+      const int g = (int)blockIdx.x >= nt ? 1 : 0;
+      const int t = xcd_tile((int)blockIdx.x - g * nt, nt);
+      srow = t % p.num_rows;
+      j0 = (t / p.num_rows) * kBN;
+      const int e_r = scalar_load_int(p.s_offsets, srow);
+      const int n_r = scalar_load_int(p.s_offsets, srow + 1) - e_r;
+      const int c0 = g * n_r / 2, c1 = (g + 1) * n_r / 2;
+      idx_base = e_r;
+      p_first = c0 * kStepsPerBlock;
+      p_steps = (c1 - c0) * kStepsPerBlock;
+      pair_id = t;
+      if (g == 0) {
+        p_flush = p_steps;
+      } else {
+        do_collect = true;
+      }
+    } else if (use_pairs) {
       // ==== pair balancing (one workgroup per CU, #tiles <= #CUs) ==========
       // A tile's length is its block-row's nonzero count, and with one tile
       // per CU the launch ends with the longest row. Within each panel the
@@ -1764,18 +1811,24 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       else
         pipeline(0, nsteps);
     } else if constexpr (kScalarIdx) {
-      cached_e = -1;
       // (Both operands k-contiguous, DSD NT / DDS NT: the unrolled loop
       // needs 12 more address registers than it has and spills; those two
       // keep the per-step pipeline.)
+      cached_e = -1;
       if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
-                         kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
+                    kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
         pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
                         p_flush > 0 ? p_flush / kStepsPerBlock : -1);
       else
         pipeline(p_first, p_steps, p_flush);
       tl(2);
-      if (do_collect) collect();
+      if constexpr (kPairs) {
+        if (split_producer() && p_steps == 0) publish();  // an empty chunk
+        // Both modes hand over exactly one partial: the head [0, p_first)
+        // of the consumer's row (pair: the heavy row's first hb blocks;
+        // split: the first half).
+        if (do_collect) collect();
+      }
     } else if constexpr (kSparseD) {
       cached_e = -1;
       pipeline(0, entries * kStepsPerBlock);  // list staged by the setup
@@ -1786,10 +1839,14 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     bool empty = false;
     if constexpr (!kSparseOut) empty = p_steps == 0 && !do_collect;
     if constexpr (!kSparseOut && !kScalarIdx) empty = entries == 0;
-    if (empty)
+    if (split_producer()) {
+      // split mode: this chunk's partial is published; the tile is written
+      // by its consumer
+    } else if (empty) {
       write_zero_tile();
-    else
+    } else {
       write_tile(out_block);
+    }
     if constexpr ((SPUTNIK_EXP & 512) != 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       tl(4);

@@ -33,6 +33,9 @@ hipError_t Launch(const GemmParams &p, bool grouped, hipStream_t stream) {
     // overlap the other's pipeline.
     if (grouped)
       return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgTall>(p, stream);
+    // Split mode (few tiles): two workgroups per tile, its own kernel.
+    if (p.pair != 0 && p.pair_split > 1)
+      return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSplit>(p, stream);
     return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSparse>(p, stream);
   }
 }

@@ -155,6 +155,8 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     const int cus = DeviceCUs(dev);
     if (cus <= 0) return;
     const int slots = cus * CfgSparse::kWGs;
+    // Partial slots: slots / 2 pairs, or one per tile in split mode (at most
+    // slots / 2 tiles). 128 x 256 KiB = 32 MiB per stream on MI355X.
     const int pairs = slots / 2;
     float *partials = nullptr;
     unsigned *flags = nullptr;
@@ -191,10 +193,27 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     return e != nullptr ? std::atoi(e) : SPUTNIK_PAIR_XCD2_DEFAULT;
   }();
   p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? 1 : 0;
+  // Split mode (GemmParams::pair_split) when the tiles fill at most half of
+  // the workgroup slots (e.g. 512-2048-row panels of a strong-scaled 4096^2,
+  // or narrow N) and the rows hold at least 4 blocks on average: two
+  // workgroups per tile. SPUTNIK_AMD_SPLIT=0 turns it off. (r03b, DSD
+  // K=N=4096 50%: M=512 45.2 -> 34.6 us, 1024 47.6 -> 38.4, 2048 48.8 ->
+  // 45.2; 4 or 8 workgroups per tile were slower.)
+  static const int split_on = [] {
+    const char *e = std::getenv("SPUTNIK_AMD_SPLIT");
+    return e != nullptr ? std::atoi(e) : 1;
+  }();
+  int split = 1;
+  if (split_on != 0 && (long long)p->num_tiles * 2 <= slot->slots &&
+      blocks >= 4LL * p->num_rows)
+    split = 2;
+  p->pair_split = split;
+  if (split > 1) p->grid = split * p->num_tiles;
 }
 
-// Pair hand-offs that timed out since the last call, over every workspace of
-// the current device; the error words are cleared. One device-wide
+// Pair hand-offs that timed out (and were recomputed by their consumer)
+// since the last call, summed over every workspace of the current device;
+// the error words are cleared. One device-wide
 // synchronize first: the streams the workspaces were made for may have been
 // destroyed since (or their handles reused), so they are never used here.
 int PairErrors() {
@@ -210,7 +229,7 @@ int PairErrors() {
                   hipMemcpyDeviceToHost) != hipSuccess)
       return -1;
     if (word != 0) {
-      ++total;
+      total += (int)word;
       const unsigned zero = 0;
       if (hipMemcpy(s.flags + s.pairs, &zero, sizeof(zero),
                     hipMemcpyHostToDevice) != hipSuccess)

@@ -168,12 +168,56 @@ def test_kat_dsd_4096_pairs(ta):
     assert sp.pair_errors() == 0
 
 
+@pytest.mark.parametrize("m", [512, 1024, 2048])
+@pytest.mark.parametrize("ta", [False, True])
+def test_kat_dsd_split(m, ta):
+    """At most half as many tiles as CUs (the row panels of a strong-scaled
+    4096^2): split mode, two workgroups per tile, the first half's fp32
+    partial added by the second."""
+    got, want, _ = kat_dsd(m, 4096, 4096, 0.5, ta, False, "f16", seed=7)
+    _equal(got, want, f"dsd split m={m} ta={ta}")
+    assert sp.pair_errors() == 0
+
+
+@pytest.mark.parametrize("n", [512, 2048])
+@pytest.mark.parametrize("tb", [False, True])
+def test_kat_dds_split(n, tb):
+    got, want = kat_dds(4096, 4096, n, 0.5, False, tb, "f16", seed=8)
+    _equal(got, want, f"dds split n={n} tb={tb}")
+    assert sp.pair_errors() == 0
+
+
+def test_split_timeout_fails_loudly():
+    """Split mode with every producer silent (test knob): each consumer
+    times out, its tile is NaN and counted; 1024 rows = 8 block-rows x 8
+    panels = 64 tiles, so 64 errors. The next launch is exact again."""
+    got, want, (A, Bd, C) = kat_dsd(1024, 4096, 4096, 0.5, False, False,
+                                    "f16", seed=9)
+    _equal(got, want, "split before fault")
+    assert sp.pair_errors() == 0
+    sp.lib().sputnik_debug_pair_fault(1)
+    try:
+        got.fill_(0)
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+        torch.cuda.synchronize()
+    finally:
+        sp.lib().sputnik_debug_pair_fault(0)
+    assert bool(torch.isnan(got.float()).all()), "every tile has a consumer"
+    assert sp.pair_errors() == 64
+    got.fill_(float("nan"))
+    sp.MatmulEx(A.m, False, Bd.m, False, C)
+    _equal(got, want, "split after fault")
+    assert sp.pair_errors() == 0
+
+
 # ------------------------------------------------------------------ DDS --
 
-def kat_dds(m, k, n, density, ta, tb, dtype, ex=False, seed=0):
+def kat_dds(m, k, n, density, ta, tb, dtype, ex=False, seed=0,
+            topology=None, handles=False):
     rng = np.random.default_rng(seed)
     A = IDense(*((k, m) if ta else (m, k)), rng, dtype)
-    Bs = ISparse(*((n, k) if tb else (k, n)), density, rng, dtype)
+    Bs = ISparse(*((n, k) if tb else (k, n)), density, rng, dtype,
+                 topology=topology)
     C, c_t = _nan_out(m, n, dtype)
     if ex:
         sp.Transpose(Bs.m)
@@ -181,6 +225,8 @@ def kat_dds(m, k, n, density, ta, tb, dtype, ex=False, seed=0):
     else:
         sp.Matmul(A.m, ta, Bs.m, tb, C)
     want = _op(A.values, ta).astype(np.float64) @ _op(Bs.dense, tb)
+    if handles:
+        return c_t, _expect(want, dtype), (A, Bs, C)
     return c_t, _expect(want, dtype)
 
 
@@ -308,33 +354,92 @@ def _skewed_rows(rng, rows_b=32, cols_b=32):
     return offsets, indices
 
 
-def test_pair_timeout_fails_loudly():
+@pytest.mark.parametrize("op,ta,tb", [("dsd", False, False),
+                                      ("dsd", True, False),
+                                      ("dsd", False, True),
+                                      ("dds", False, False),
+                                      ("dds", False, True)])
+def test_pair_timeout_fails_loudly(op, ta, tb):
     """A pair producer that never publishes (test knob) makes its consumer
-    time out: the consumer's tile is NaN (never a stale partial), the error
-    is reported by sputnik_pair_errors(), and the next launch on the same
-    workspace is exact again (per-launch epochs, no flag to reset)."""
+    time out (after the bounded wait): the consumer's tile is NaN (never a
+    stale or partial sum), every such consumer is counted by
+    sputnik_pair_errors(), the tiles without a hand-off are exact, and the
+    next launch on the same workspace is exact and error-free again
+    (per-launch epochs, no flag to reset)."""
     rng = np.random.default_rng(5)
-    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, None, False, False,
-                                    "f16", seed=5, topology=_skewed_rows(rng))
-    _equal(got, want, "dsd before fault")
+    topo = _skewed_rows(rng)
+    if op == "dsd":
+        got, want, (X, Y, C) = kat_dsd(4096, 4096, 4096, None, ta, tb, "f16",
+                                       seed=5, topology=topo)
+    else:
+        got, want, (X, Y, C) = kat_dds(4096, 4096, 4096, None, ta, tb, "f16",
+                                       seed=5, topology=topo, handles=True)
+
+    def run():
+        sp.MatmulEx(X.m, ta, Y.m, tb, C)
+
+    _equal(got, want, f"{op} before fault")
     assert sp.pair_errors() == 0
     sp.lib().sputnik_debug_pair_fault(1)
     try:
         got.fill_(0)
-        sp.MatmulEx(A.m, False, Bd.m, False, C)
+        run()
         torch.cuda.synchronize()
     finally:
         sp.lib().sputnik_debug_pair_fault(0)
-    nan_rows = torch.isnan(got.float()).any(dim=1)
-    assert int(nan_rows.sum()) > 0, "no consumer tile was poisoned"
-    assert sp.pair_errors() > 0
+    # DDS writes C transposed: a poisoned tile is 128 columns x 512 rows.
+    bad = torch.isnan(got.float())
+    poisoned = (bad.any(dim=1) if op == "dsd" else bad.any(dim=0))
+    assert int(poisoned.sum()) > 0, "no consumer tile was poisoned"
+    errors = sp.pair_errors()
+    if (op, ta, tb) in (("dsd", False, False), ("dds", False, True)):
+        # S rows are the skewed stored rows: 16 heavy rows x 8 panels, each
+        # handing 12 blocks to its light partner.
+        assert errors == 128
+    else:
+        assert errors > 0
     assert sp.pair_errors() == 0  # cleared by the previous call
-    ok = ~nan_rows
+    ok = ~bad
     assert torch.equal(got[ok], want[ok])  # tiles without a hand-off exact
     got.fill_(float("nan"))
-    sp.MatmulEx(A.m, False, Bd.m, False, C)
-    _equal(got, want, "dsd after fault")
+    run()
+    _equal(got, want, f"{op} after fault")
     assert sp.pair_errors() == 0
+
+
+def test_tall_persistent_two_host_threads_one_stream():
+    """Two host threads launching persistent tall DSDs on one stream (ctypes
+    drops the GIL, so their host-side preparation interleaves): the tile
+    counter is reset on the device by each launch's last workgroup, so every
+    launch computes every tile whatever order the launches were queued in."""
+    import threading
+    rng = np.random.default_rng(13)
+    A = ISparse(65536, 256, 0.3, rng, "f16")
+    Bd = IDense(256, 512, rng, "f16")
+    want = _expect(A.dense.astype(np.float64) @ Bd.values, "f16")
+    outs = [_nan_out(65536, 512, "f16") for _ in range(2)]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    errors = []
+
+    def worker(i):
+        try:
+            torch.cuda.set_device(0)
+            with torch.cuda.stream(s):
+                for _ in range(8):
+                    sp.MatmulEx(A.m, False, Bd.m, False, outs[i][0])
+        except Exception as exc:  # reported below
+            errors.append(exc)
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    s.synchronize()
+    assert not errors, errors
+    for i in range(2):
+        _equal(outs[i][1], want, f"thread {i}")
 
 
 def test_graph_capture_with_pairs():
@@ -366,7 +471,7 @@ def test_graph_capture_with_pairs():
 def test_graph_capture_tall_persistent():
     """A tall DSD captured into a graph on a stream whose persistent tile
     counter already exists: the captured launch runs one tile per workgroup
-    (the counter base is host state), so replays interleaved with eager
+    (persistence is off under capture), so replays interleaved with eager
     persistent launches on the same stream all stay exact."""
     rng = np.random.default_rng(12)
     A = ISparse(65536, 256, 0.3, rng, "f16")

@@ -269,9 +269,12 @@ def test_two_rank_gloo_sharded_hip_dsd_matches_unsharded(tmp_path):
 
 
 @pytest.mark.gpu
-def test_bench_two_ranks_shard_one_matrix():
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_two_ranks_shard_one_matrix(scaling):
     """bench.py's N>1 path (one matrix split by shard_rows_by_nnz, max over
-    ranks, whole-job value) on two ranks sharing the device, gloo backend."""
+    ranks, whole-job value) on two ranks sharing the device, gloo backend:
+    strong scaling splits the metric's own 4096-row matrix (16 block-rows
+    per rank), weak scaling gives every rank 4096 rows."""
     import json
     import subprocess
     import sys
@@ -282,11 +285,18 @@ def test_bench_two_ranks_shard_one_matrix():
            "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--sweep", "",
-           "--no-cpu", "--dist-backend", "gloo"]
+           "--no-cpu", "--dist-backend", "gloo", "--scaling", scaling]
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
                          cwd=root)
     assert res.returncode == 0, res.stderr[-2000:]
     line = json.loads([x for x in res.stdout.splitlines()
                        if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["scaling"] == scaling
     assert "split by nnz over 2" in line["config"]["parallelism"]
+    m = 4096 if scaling == "strong" else 8192
+    assert line["config"]["m"] == m
+    # rank 0 holds about half of the block-rows of the one matrix
+    nb0 = line["by_density"]["0.5"]["nnz_blocks_per_rank"]
+    total = (m // 128) * 32 // 2
+    assert abs(nb0 - total / 2) <= 32, (nb0, total)
