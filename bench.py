@@ -66,10 +66,18 @@ def parse():
                          "has settled (the reference used 10 short calls)")
     ap.add_argument("--workload", default="dsd",
                     choices=["dsd", "sdd_dds", "moe", "panel", "op",
-                             "transpose"],
+                             "transpose", "sweep"],
                     help="dsd: the headline metric (BASELINE config 2); "
                          "sdd_dds: config 3; moe: config 4; panel: config 5; "
                          "op: one product/transpose; transpose: metadata")
+    ap.add_argument("--graph", action="store_true",
+                    help="time replays of a hipGraph captured around one step "
+                         "(captured launches run without pair hand-offs and "
+                         "persistent tile fetch: dispatch.cpp)")
+    ap.add_argument("--sweep-ops", default="dsd,dds,sdd")
+    ap.add_argument("--sweep-dims", default="512,1024,2048,4096,8192,16384")
+    ap.add_argument("--sweep-densities", default="1.0,0.5,0.1,0.01")
+    ap.add_argument("--sweep-trans", default="NN,NT,TN,TT")
     ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"])
     ap.add_argument("--trans", default="NN", choices=["NN", "NT", "TN", "TT"])
     ap.add_argument("--api", default="ex", choices=["ex", "matmul"])
@@ -259,6 +267,28 @@ def barrier(world):
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+
+
+def graph_step(prob):
+    """One step of `prob` captured into a hipGraph (torch.cuda.CUDAGraph) on
+    a side stream: the launcher is built on that stream, so the library's
+    launches go into the capture. The returned callable replays it on the
+    current stream."""
+    import torch
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn = prob.launcher()  # binds s; runs once eagerly (workspaces exist)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        codes = fn()
+    torch.cuda.synchronize()
+    codes = codes if isinstance(codes, tuple) else (codes,)
+    if any(c != 0 for c in codes):
+        raise RuntimeError(f"launch inside graph capture returned {codes}")
+    prob._graph = (g, fn)  # keep the captured arguments alive
+    return g.replay
 
 
 def time_steps(fn, steps, warmup, world):
@@ -555,7 +585,7 @@ class OpProblem:
             sp.RowIndices(self.S, self.S.row_indices)
         self.op, self.ta, self.tb, self.api = op, ta, tb, args.api
         self.flops = 2.0 * nz * d
-        self.anchor_shape = (d, d, int(round(d * dens)))
+        self.anchor_shape = (d, d, max(8, int(round(d * dens))))
         meta_t = (op == "dsd" and ta) or (op == "dds" and not tb)
         meta = (d // BLOCK + 1) * 4 + nb * (6 if meta_t else 2)
         self.bytes = (nz * 2 + meta + d * d * 2 * (2 if op == "sdd" else 1) +
@@ -627,6 +657,48 @@ class TransposeProblem:
         return lambda: L.sputnik_transpose(ctypes.byref(c), stream)
 
 
+def run_sweep(args, device, build):
+    """The reference benchmark grid (dsd_benchmark.cu:32-46 and its dds /
+    sdd siblings): dims x densities x transposes per product, MatmulEx
+    (metadata precomputed), fp16, one JSON line per point with the
+    hipBLASLt dense GEMM of the same FLOPs beside it (density 1.0 is the
+    exact dense comparison)."""
+    import argparse as _ap
+    import torch
+    for op in [o for o in args.sweep_ops.split(",") if o]:
+        for d in [int(x) for x in args.sweep_dims.split(",") if x]:
+            for dens in [float(x) for x in args.sweep_densities.split(",") if x]:
+                anchor = None
+                for tr in [t for t in args.sweep_trans.split(",") if t]:
+                    a = _ap.Namespace(**vars(args))
+                    a.op, a.trans, a.api, a.density = op, tr, "ex", dens
+                    a.k = a.m = a.n = d
+                    try:
+                        prob = OpProblem(a, device)
+                        fn = prob.launcher()
+                        ms = time_steps(fn, args.steps, args.warmup, 1)
+                    except (RuntimeError, AssertionError) as exc:
+                        emit({"op": op, "trans": tr, "dim": d, "density": dens,
+                              "error": str(exc)[:200]})
+                        torch.cuda.empty_cache()
+                        continue
+                    per = ms / args.steps
+                    tflops = prob.flops / (per * 1e-3) / 1e12
+                    if anchor is None:
+                        anchor = dense_anchor(*prob.anchor_shape, args.dtype,
+                                              device, iters=20)
+                    emit({"op": op, "trans": tr, "dim": d, "density": dens,
+                          "nnz_blocks": int(prob.S.nonzeros) // (BLOCK * BLOCK),
+                          "us": round(per * 1e3, 2),
+                          "tflops": round(tflops, 2),
+                          "dense_anchor_tflops": anchor.get("tflops"),
+                          "sparse_over_dense": round(tflops / anchor["tflops"], 3)
+                          if "tflops" in anchor else None,
+                          "build": build.get("hash")})
+                    del prob, fn
+                    torch.cuda.empty_cache()
+
+
 def emit(line):
     print(json.dumps(line))
     sys.stdout.flush()
@@ -658,7 +730,7 @@ def run_other(args, world, rank, device, build):
         metric = "effective TFLOP/s (nnz-FLOPs) row-panel DSD M=131072 K=N=4096 2%"
         scaling = "strong"
         prob.anchor_shape = (prob.m, args.n, int(round(args.k * 0.02)))
-    fn = prob.launcher()
+    fn = graph_step(prob) if args.graph else prob.launcher()
     ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
     per = ms / args.steps
     flops_all = sum_over_ranks(prob.flops, world)
@@ -708,7 +780,7 @@ def run_other(args, world, rank, device, build):
               "scaling": scaling, "vs_baseline": None,
               "dtype": getattr(prob, "dtype_name", args.dtype),
               "data": "synthetic", "config": {"workload": prob.desc},
-              "build": build})
+              "graph": args.graph, "build": build})
 
 
 def main():
@@ -740,6 +812,9 @@ def main():
         import sputnik_amd as sp
         build = {"hash": sp.build_hash()}
 
+    if args.workload == "sweep":
+        run_sweep(args, device, build)
+        return
     if args.workload != "dsd":
         run_other(args, world, rank, device, build)
         if world > 1:
@@ -755,7 +830,7 @@ def main():
     m_total = args.m if args.scaling == "strong" else args.m * world
     for d in densities:
         prob = dsd_panel(args, world, rank, device, d, m_total=m_total)
-        fn = prob.launcher()
+        fn = graph_step(prob) if args.graph else prob.launcher()
         ms = max_over_ranks(time_steps(fn, args.steps, args.warmup, world), world)
         per_step = ms / args.steps
         flops_all = sum_over_ranks(prob.flops, world)
@@ -821,6 +896,7 @@ def main():
             "dense_anchor": anchor,
             "cpu_baseline": cpu,
             "config1": config1,
+            "graph": args.graph,
             "build": build,
         })
 
