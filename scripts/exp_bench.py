@@ -24,12 +24,29 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--op", default="dsd",
-                    choices=["dsd", "sdd", "moe_sdd", "moe_dsd", "pair", "moe"])
+                    choices=["dsd", "sdd", "moe_sdd", "moe_dsd", "pair", "moe", "op"])
+    # --op op: one product of bench.OpProblem (square dims = --k), MatmulEx.
+    ap.add_argument("--xop", default="dsd", choices=["dsd", "dds", "sdd"])
+    ap.add_argument("--trans", default="NN")
     args = ap.parse_args()
     import torch
     import bench
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    if args.op == "op":
+        import sputnik_amd as sp
+        a = argparse.Namespace(op=args.xop, trans=args.trans, api="ex",
+                               density=args.density, k=args.k, m=args.k,
+                               n=args.k, dtype=args.dtype, seed=0)
+        prob = bench.OpProblem(a, dev)
+        fns = []
+        for path in args.libs:
+            sp._lib = None
+            sp.LIB_PATH = os.path.abspath(path)
+            launch = prob.launcher()
+            fns.append((os.path.basename(path), lambda f=launch: f(), ()))
+        args.op = f"{args.xop}_{args.trans}"
+        return report(args, prob, fns)
     if args.op in ("pair", "moe"):
         # Whole BASELINE workloads (config 3 / config 4) through bench.py's
         # own launchers, one per variant library.

@@ -6,7 +6,8 @@ import re
 import subprocess
 import sys
 
-SRC = "sputnik_amd/csrc/block_gemm.hip"
+import os
+SRC = os.environ.get("KRES_SRC", "sputnik_amd/csrc/block_gemm.hip")
 
 
 def short(name):

@@ -34,8 +34,13 @@ hipError_t Launch(const GemmParams &p, bool grouped, hipStream_t stream) {
     if (grouped)
       return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgTall>(p, stream);
     // Split mode (few tiles): two workgroups per tile, its own kernel.
-    if (p.pair != 0 && p.pair_split > 1)
+    if (p.pair != 0 && p.pair_split > 1) {
+      if (p.split_bn == 128)
+        return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSplit128>(p, stream);
+      if (p.split_bn == 256)
+        return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSplit256>(p, stream);
       return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSplit>(p, stream);
+    }
     return LaunchCfg<T, false, kSKC, kDKC, kOutT, CfgSparse>(p, stream);
   }
 }

@@ -203,10 +203,29 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     const char *e = std::getenv("SPUTNIK_AMD_SPLIT");
     return e != nullptr ? std::atoi(e) : 1;
   }();
+  // Tile width: the narrowest of 512 / 256 / 128 columns whose tiles (two
+  // workgroups each) still fit the slots, so a panel of few block-rows
+  // fills the CUs (r03: M = 512 on 128-column tiles, M = 1024 on 256).
   int split = 1;
   if (split_on != 0 && (long long)p->num_tiles * 2 <= slot->slots &&
-      blocks >= 4LL * p->num_rows)
+      blocks >= 4LL * p->num_rows) {
     split = 2;
+    int bn = CfgSparse::kBN;
+    for (int cand : {256, 128}) {
+      const long long tiles =
+          (long long)p->num_rows * ((p->j_limit + cand - 1) / cand);
+      if (tiles * 2 > slot->slots) break;
+      bn = cand;
+    }
+    static const int max_narrow = [] {  // tuning: 512 keeps the wide tile
+      const char *e = std::getenv("SPUTNIK_AMD_SPLIT_MIN_BN");
+      return e != nullptr ? std::atoi(e) : 128;
+    }();
+    if (bn < max_narrow) bn = max_narrow;
+    p->split_bn = bn;
+    p->num_jtiles = (p->j_limit + bn - 1) / bn;
+    p->num_tiles = p->num_rows * p->num_jtiles;
+  }
   p->pair_split = split;
   if (split > 1) p->grid = split * p->num_tiles;
 }

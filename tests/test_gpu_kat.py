@@ -169,13 +169,25 @@ def test_kat_dsd_4096_pairs(ta):
 
 
 @pytest.mark.parametrize("m", [512, 1024, 2048])
-@pytest.mark.parametrize("ta", [False, True])
-def test_kat_dsd_split(m, ta):
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False),
+                                   (False, True), (True, True)])
+def test_kat_dsd_split(m, ta, tb):
     """At most half as many tiles as CUs (the row panels of a strong-scaled
     4096^2): split mode, two workgroups per tile, the first half's fp32
-    partial added by the second."""
-    got, want, _ = kat_dsd(m, 4096, 4096, 0.5, ta, False, "f16", seed=7)
-    _equal(got, want, f"dsd split m={m} ta={ta}")
+    partial added by the second; tiles of 128 (m=512), 256 (m=1024) or 512
+    (m=2048) columns."""
+    got, want, _ = kat_dsd(m, 4096, 4096, 0.5, ta, tb, "f16", seed=7)
+    _equal(got, want, f"dsd split m={m} ta={ta} tb={tb}")
+    assert sp.pair_errors() == 0
+
+
+@pytest.mark.parametrize("m,n", [(512, 1000), (1024, 264)])
+@pytest.mark.parametrize("ta", [False, True])
+def test_kat_dsd_split_partial_tiles(m, n, ta):
+    """Split mode on narrow tiles with a partial last tile (N % 128 != 0):
+    K = 1024 at density 1 gives 8 blocks per row (split needs >= 4)."""
+    got, want, _ = kat_dsd(m, 1024, n, 1.0, ta, False, "f16", seed=10)
+    _equal(got, want, f"dsd split m={m} n={n} ta={ta}")
     assert sp.pair_errors() == 0
 
 
@@ -189,8 +201,9 @@ def test_kat_dds_split(n, tb):
 
 def test_split_timeout_fails_loudly():
     """Split mode with every producer silent (test knob): each consumer
-    times out, its tile is NaN and counted; 1024 rows = 8 block-rows x 8
-    panels = 64 tiles, so 64 errors. The next launch is exact again."""
+    times out, its tile is NaN and counted; 1024 rows = 8 block-rows on
+    256-column tiles x 16 = 128 tiles, so 128 errors. The next launch is
+    exact again."""
     got, want, (A, Bd, C) = kat_dsd(1024, 4096, 4096, 0.5, False, False,
                                     "f16", seed=9)
     _equal(got, want, "split before fault")
@@ -203,7 +216,7 @@ def test_split_timeout_fails_loudly():
     finally:
         sp.lib().sputnik_debug_pair_fault(0)
     assert bool(torch.isnan(got.float()).all()), "every tile has a consumer"
-    assert sp.pair_errors() == 64
+    assert sp.pair_errors() == 128
     got.fill_(float("nan"))
     sp.MatmulEx(A.m, False, Bd.m, False, C)
     _equal(got, want, "split after fault")
