@@ -5,7 +5,7 @@
 #   smoke -> pytest -m gpu (junit) -> the driver's bench command
 #   (--steps 20 --warmup 5) -> rocprofv3 kernel trace of that same command
 #   (timed dispatches extracted by scripts/trace_headline.py) -> PMC passes
-#   (scripts/pmc.sh) -> optional interleaved A/B of build/exp/*.so.
+#   (scripts/pmc.sh; config 3 and 5 by scripts/pmc_workload.sh) -> optional interleaved A/B of build/exp/*.so.
 # Usage: scripts/gpu_session.sh TAG [tests=1] [pmc densities or -] [ab densities or -]
 set -u
 TAG=$1; TESTS=${2:-1}; PMC=${3:-"0.5 0.1 0.3 0.9"}; AB=${4:--}
@@ -44,6 +44,10 @@ python3 scripts/trace_headline.py $OUT/prof_driver $OUT/prof_driver.log 5 20 \
   $OUT/headline_trace.json
 if [ "$PMC" != "-" ]; then
   bash scripts/pmc.sh $TAG "$PMC"; rc=$?
+  fatal $rc && exit $rc
+  bash scripts/pmc_workload.sh $TAG sdd_dds "--workload sdd_dds"; rc=$?
+  fatal $rc && exit $rc
+  bash scripts/pmc_workload.sh $TAG panel "--workload panel"; rc=$?
   fatal $rc && exit $rc
 fi
 if [ "$AB" != "-" ]; then

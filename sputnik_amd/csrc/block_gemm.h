@@ -76,18 +76,6 @@
 #endif
 // DSD / DDS staggered pipeline unrolled by one stored block (constant ring
 // slots, branch-free steady state); 0 = the generic per-step pipeline.
-#ifndef SPUTNIK_KC_ASM
-#define SPUTNIK_KC_ASM 0
-#endif
-#ifndef SPUTNIK_DKC_ONE_OFF
-#define SPUTNIK_DKC_ONE_OFF 0
-#endif
-#ifndef SPUTNIK_NT_REMAT
-#define SPUTNIK_NT_REMAT 0
-#endif
-#ifndef SPUTNIK_NT_BLOCKS
-#define SPUTNIK_NT_BLOCKS 0
-#endif
 #ifndef SPUTNIK_BLOCK_LOOP
 #define SPUTNIK_BLOCK_LOOP 1
 #endif
@@ -272,42 +260,6 @@ __device__ __forceinline__ s16x8 read_kc(const char *img, int row0, int kk,
   const int c = 4 * kk + (lane >> 4);
   return *reinterpret_cast<const s16x8 *>(
       img + row * kRowBytes + ((c ^ kc_key<kRowBytes / 16>(row)) << 4));
-}
-
-// read_kc as inline asm from one per-operand lane address: fragment f of a
-// step is the same lane pattern 16 rows further down (row0 % 16 == 0 keeps
-// the swizzle key a function of the lane alone), so it is the instruction's
-// immediate offset f * 16 * kRowBytes. Nothing per fragment stays live
-// across steps, and, being asm, the reads are ordered like read_mn's (the
-// caller owns the lgkmcnt wait).
-template <int kRowBytes>
-__device__ __forceinline__ uint32_t kc_lane_addr(const char *img, int row0,
-                                                 int kk, int lane) {
-  const int r = lane & 15;
-  const int c = 4 * kk + (lane >> 4);
-  return (uint32_t)(uintptr_t)(
-             (__attribute__((address_space(3))) const char *)(img)) +
-         (uint32_t)(row0 * kRowBytes + r * kRowBytes +
-                    ((c ^ kc_key<kRowBytes / 16>(r)) << 4));
-}
-template <int kOff>
-__device__ __forceinline__ s16x8 ds_read128(uint32_t addr) {
-  s16x8 out;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(out) : "v"(addr), "n"(kOff));
-  return out;
-}
-template <int kStride>
-__device__ __forceinline__ s16x8 ds_read128_f(uint32_t addr, int f) {
-  switch (f) {  // f is a constant after unrolling
-    case 0: return ds_read128<0>(addr);
-    case 1: return ds_read128<kStride>(addr);
-    case 2: return ds_read128<2 * kStride>(addr);
-    case 3: return ds_read128<3 * kStride>(addr);
-    case 4: return ds_read128<4 * kStride>(addr);
-    case 5: return ds_read128<5 * kStride>(addr);
-    case 6: return ds_read128<6 * kStride>(addr);
-    default: return ds_read128<7 * kStride>(addr);
-  }
 }
 
 // Same fragment from an m/n-contiguous image [64 k][cols] (kRowBytes per
@@ -599,11 +551,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   // Grouped SDD: block j of the tile (j < grp_count) takes the D columns
   // grp_col[j] .. +127; lanes of absent blocks read zeros.
   static_assert(kGrp <= 4, "grouped SDD: at most 4 blocks per tile");
-  // k-contiguous D of DSD NT / DDS NT: one lane offset for all D DMA
-  // instructions of a step (fire()); d_end = end of row j_limit - 1.
-  constexpr bool kDOneOff = SPUTNIK_DKC_ONE_OFF != 0 && kDKC && !kDenseS &&
-                            !kSparseD;
-  const char *d_end = nullptr;
   long long grp_b0 = 0;   // SDD: first output block of the tile
   int grp_count = 1;      // SDD: blocks in the tile
   int grp_c0 = 0, grp_c1 = 0, grp_c2 = 0, grp_c3 = 0;  // D column origins
@@ -611,14 +558,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     return jb == 0 ? grp_c0 : jb == 1 ? grp_c1 : jb == 2 ? grp_c2 : grp_c3;
   };
   auto setup_d = [&](int j0) {
-    if constexpr (kDOneOff) {
-      // q = 0 only; rows 16 q on come from fire()'s per-instruction bases.
-      const int j = kKcRowsPerInstr * (wave * kDInstr) + lane / kKcChunks;
-      const int c = (lane % kKcChunks) ^ kc_key<kKcChunks>(j);
-      d_off[0] = (uint32_t)(j * p.d_ld + c * 16);
-      d_end = p.d_data + (long long)p.j_limit * p.d_ld;
-      return;
-    }
 #pragma unroll
     for (int q = 0; q < kDInstr; ++q) {
       const int g = wave * kDInstr + q;
@@ -768,51 +707,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     char *slot_base = lds + slot * kStageBytes;
     const __amdgpu_buffer_rsrc_t rs = make_rsrc(s_base);
     const __amdgpu_buffer_rsrc_t rd = make_rsrc(d_base);
-    // NT remat: the lane offsets are recomputed from the lane id at each
-    // use instead of living across the loop (4 fewer long-lived VGPRs).
-    int rl = lane;
-    if constexpr (kDOneOff && SPUTNIK_NT_REMAT != 0) {
-      rl = threadIdx.x;
-      asm volatile("" : "+v"(rl));
-      rl &= 63;
-    }
 #pragma unroll
     for (int q = 0; q < kSInstr; ++q) {
       uint32_t off = s_off[q];
-      if constexpr (kDOneOff && SPUTNIK_NT_REMAT != 0) {
-        const int row = kKcRowsPerInstr * (wave * kSInstr + q) + rl / kKcChunks;
-        const int c = (rl % kKcChunks) ^ kc_key<kKcChunks>(row);
-        off = (uint32_t)(row * 256 + c * 16);
-      }
       if constexpr (kDenseS) off = s_lk[q] < krem ? off : kOOB;
       dma16<kDenseS ? 0 : SPUTNIK_S_AUX>(
           rs, slot_base + (wave * kSInstr + q) * 1024, off);
-    }
-    if constexpr (kDOneOff) {
-      // k-contiguous D: instruction q reads rows 16 q further down with the
-      // same lane offset, so it gets its own descriptor (base 16 q rows on,
-      // records up to the end of row j_limit - 1: the range check masks the
-      // rows past j_limit) and one VGPR offset serves all kDInstr of them.
-      const long long q_bytes = (long long)kKcRowsPerInstr * p.d_ld;
-      uint32_t doff = d_off[0];
-      if constexpr (SPUTNIK_NT_REMAT != 0) {
-        const int j = kKcRowsPerInstr * (wave * kDInstr) + rl / kKcChunks;
-        const int c = (rl % kKcChunks) ^ kc_key<kKcChunks>(j);
-        doff = (uint32_t)(j * p.d_ld + c * 16);
-      }
-#pragma unroll
-      for (int q = 0; q < kDInstr; ++q) {
-        const char *bq = d_base + q * q_bytes;
-        const long long left = d_end - bq;
-        const uint32_t nr = left <= 0 ? 0u
-                            : left >= (long long)kNumRecords ? kNumRecords
-                                                             : (uint32_t)left;
-        dma16<SPUTNIK_D_AUX>(
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(bq), 0, nr,
-                                              0x00020000),
-            slot_base + kSBytes + (wave * kDInstr + q) * 1024, doff);
-      }
-      return;
     }
 #pragma unroll
     for (int q = 0; q < kDInstr; ++q) {
@@ -841,26 +741,6 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
     asm volatile("" : "+s"(slot_off));
     const char *simg = lds + slot_off;
     const char *dimg = simg + kSBytes;
-    if constexpr (SPUTNIK_KC_ASM != 0 && kSKC && kDKC) {
-      int rl = lane;
-      if constexpr (SPUTNIK_NT_REMAT != 0) {
-        rl = threadIdx.x;
-        asm volatile("" : "+v"(rl));
-        rl &= 63;
-      }
-#pragma unroll
-      for (int kk = 0; kk < kKK; ++kk) {
-        const uint32_t sa = kc_lane_addr<kKcRow>(simg, row_w, kk0 + kk, rl);
-        const uint32_t da = kc_lane_addr<kKcRow>(dimg, col_w, kk0 + kk, rl);
-#pragma unroll
-        for (int f = 0; f < kFM; ++f)
-          F.a[kk][f] = ds_read128_f<16 * kKcRow>(sa, f);
-#pragma unroll
-        for (int f = 0; f < kFN; ++f)
-          F.b[kk][f] = ds_read128_f<16 * kKcRow>(da, f);
-      }
-      return;
-    }
 #pragma unroll
     for (int kk = 0; kk < kKK; ++kk) {
 #pragma unroll
@@ -1941,7 +1821,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       // keep the per-step pipeline.)
       cached_e = -1;
       if constexpr (SPUTNIK_BLOCK_LOOP != 0 && Cfg::kStagger &&
-                    kStages == 4 && kStepsPerBlock == 4 && (SPUTNIK_NT_BLOCKS || !(kSKC && kDKC)))
+                    kStages == 4 && kStepsPerBlock == 4 && !(kSKC && kDKC))
         pipeline_blocks(p_first / kStepsPerBlock, p_steps / kStepsPerBlock,
                         p_flush > 0 ? p_flush / kStepsPerBlock : -1);
       else
