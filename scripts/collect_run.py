@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""Copy one scripts/gpu_measure.sh run from gpurun_out/TAG into the tracked
-profiles/r02/TAG: each step's JSON line, the rocprofv3 kernel stats of the
-headline, the step log, and the junit summary (profiles/r02_gputest_summary.json).
+"""Copy one scripts/gpu_session.sh (or gpu_measure.sh) run from gpurun_out/TAG
+into the tracked profiles/rNN/TAG (NN from the tag's first three characters):
+each step's JSON line, the rocprofv3 kernel stats of the driver's command and
+of the headline, the timed-dispatch extract (headline_trace.json), the PMC
+summaries, the step log, and the junit summary.
 Usage: scripts/collect_run.py TAG"""
 import json
+import re
 import os
 import shutil
 import subprocess
@@ -15,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     tag = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", tag)
-    dst = os.path.join(ROOT, "profiles", "r02", tag)
+    rnd = tag[:3] if re.match(r"r\d\d", tag) else "r02"
+    dst = os.path.join(ROOT, "profiles", rnd, tag)
     os.makedirs(dst, exist_ok=True)
     for f in sorted(os.listdir(src)):
         if not f.endswith(".log") or f in ("smoke.log", "pytest_gpu.log",
@@ -29,6 +33,12 @@ def main():
     ks = os.path.join(src, "prof", "run_kernel_stats.csv")
     if os.path.exists(ks):
         shutil.copy(ks, os.path.join(dst, "dsd4096_d50_kernel_stats.csv"))
+    ks = os.path.join(src, "prof_driver", "run_kernel_stats.csv")
+    if os.path.exists(ks):
+        shutil.copy(ks, os.path.join(dst, "driver_kernel_stats.csv"))
+    for f in ("headline_trace.json", "pmc_sdd_dds.json", "pmc_panel.json"):
+        if os.path.exists(os.path.join(src, f)):
+            shutil.copy(os.path.join(src, f), dst)
     for w in ("sdd_dds", "panel"):
         ks = os.path.join(src, "prof_" + w, "run_kernel_stats.csv")
         if os.path.exists(ks):
@@ -42,8 +52,7 @@ def main():
         subprocess.check_call([sys.executable,
                                os.path.join(ROOT, "scripts", "junit_summary.py"),
                                junit,
-                               os.path.join(ROOT, "profiles",
-                                            "r02_gputest_summary.json"), tag])
+                               os.path.join(dst, "gputest_summary.json"), tag])
     print("collected", tag, "->", dst)
 
 
