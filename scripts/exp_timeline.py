@@ -165,7 +165,24 @@ def main():
         torch.cuda.synchronize()
         fn()
         torch.cuda.synchronize()
-        res = summarize(buf.cpu().numpy(), 32768)
+        host = buf.cpu().numpy()
+        if os.environ.get("TIMELINE_SEG"):
+            # SPUTNIK_EXP & 128 builds: per-segment shader-cycle sums of the
+            # k-loop for waves 0 (leading half) and kNW/2 (lagging half) of
+            # each workgroup at debug + 2048*16 + 16 b + {0, 8}.
+            res = summarize(host, 2048)
+            seg = host[2048 * 16:4096 * 16].reshape(2048, 2, 8)[:, :, :6]
+            steps = host[:2048 * 16].reshape(2048, 16)[:, 7]
+            live = steps > 0
+            names_ = ["wait_b1", "dma_issue", "read_issue", "b2",
+                      "mfma_issue", "read_wait"]
+            res["segments_per_step"] = {
+                half: {n: round(float(np.median(seg[live, h, q] /
+                                                 steps[live])), 1)
+                       for q, n in enumerate(names_)}
+                for h, half in enumerate(("lead", "lag"))}
+        else:
+            res = summarize(host, 32768)
         res["workload"] = name
         print(json.dumps(res), flush=True)
         del keep

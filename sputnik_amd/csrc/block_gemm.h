@@ -1147,6 +1147,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       constexpr int H = decltype(h_c)::value;
       constexpr bool LAST = decltype(last_c)::value;
       constexpr bool kHasNext = !(LAST && H == 3);        // i + 1 < s
+      SEG_STAMP(0);
       if constexpr (kHasNext) {
         if (!L) {
           if constexpr (LAST && H == 2)
@@ -1155,6 +1156,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
             wait_vmcnt<kGroup>();
         }
         __builtin_amdgcn_s_barrier();
+        SEG_STAMP(1);
         if constexpr (kDenseS) {
           if constexpr (H == 0 || !LAST) {                  // step i + 3
             prep(4 * b + H + 3);
@@ -1169,7 +1171,9 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
           }
           fire_sub(H - 1, H - 1);
         }
+        SEG_STAMP(2);
         read_step((H + 1) & 3, next);
+        SEG_STAMP(3);
       }
       if (L) {
         if constexpr (!LAST || H == 0)
@@ -1178,8 +1182,12 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
           wait_vmcnt<0>();
       }
       __builtin_amdgcn_s_barrier();
+      SEG_STAMP(4);
       mfma_step(cur);
+      SEG_STAMP(5);
       if constexpr (kHasNext) wait_step(next);
+      SEG_STAMP(6);
+      SEG_ACCUM();
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
