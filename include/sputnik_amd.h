@@ -169,6 +169,12 @@ int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
 int sputnik_pair_errors(void);
 /* Test knob: when on, pair producers never publish (forces the timeout). */
 void sputnik_debug_pair_fault(int on);
+/* Workspaces made for launches captured into graphs on the current device
+ * (pair-balancing workspaces + persistent tile counters). A captured launch
+ * gets one per (capture, capturing stream), kept for the process's life; a
+ * graph therefore must not be replayed concurrently with a second
+ * instantiation of the same capture. Host-only query. */
+int sputnik_capture_workspaces(void);
 
 #ifdef __cplusplus
 }  /* extern "C" */

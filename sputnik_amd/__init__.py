@@ -115,6 +115,7 @@ _SIGNATURES = {
     "sputnik_sdd_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P],
     "sputnik_pair_errors": [],
     "sputnik_debug_pair_fault": [ctypes.c_int],
+    "sputnik_capture_workspaces": [],
 }
 _RESTYPES = {
     "sputnik_abi_block_matrix_size": ctypes.c_size_t,
@@ -364,6 +365,12 @@ def pair_errors() -> int:
     return int(lib().sputnik_pair_errors())
 
 
+def capture_workspaces() -> int:
+    """Workspaces made for graph-captured launches on the current device
+    (sputnik_capture_workspaces() in include/sputnik_amd.h)."""
+    return int(lib().sputnik_capture_workspaces())
+
+
 def build_hash() -> str:
     return lib().sputnik_build_hash().decode()
 
@@ -413,7 +420,7 @@ def version() -> str:
 __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
-    "build_hash", "pair_errors", "sdd_plan",
+    "build_hash", "capture_workspaces", "pair_errors", "sdd_plan",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",

@@ -57,6 +57,7 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
 // makes every pair producer skip its publish.
 int PairErrors();
 void SetPairFault(int on);
+int CaptureWorkspaces();
 
 }  // namespace sputnik_amd
 

@@ -164,6 +164,14 @@ struct GemmParams {
   unsigned *pair_flags;        // #pairs; holds the epoch of the launch whose
                                // producer published last (never reset)
   unsigned pair_epoch;         // this launch's epoch (never 0)
+  // Launches captured into a graph replay one set of arguments, so their
+  // epoch lives on the device: pair_sync = [epoch word, arrival count] of
+  // the capture's own workspace. Every workgroup reads the epoch word at
+  // its start and uses (word mod 2^31) + 1; each adds 1 to the arrival count
+  // as it exits, and the last one (every other workgroup has read the word)
+  // resets the count and advances the word for the next replay. nullptr:
+  // eager launch, the host's pair_epoch.
+  unsigned *pair_sync;
   unsigned *pair_error;        // += 1 per consumer that timed out
   int pair_fault;              // test knob: producers never publish
   // Pair launches with 8 panels: XCD x (= workgroup b mod 8) takes panels
@@ -830,6 +838,16 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
   constexpr int kSc1 = 16;  // cache-policy bits: sc1
   int pair_id = 0;
   int pair_target = 0;  // blocks per workgroup the pair schedule aims at
+  unsigned pair_epoch = p.pair_epoch;
+  if constexpr (kPairs) {
+    // Captured launch: the epoch word was last written by the previous
+    // launch's last workgroup (kernel boundary: the scalar cache starts
+    // clean), so a scalar load sees it.
+    if (p.pair != 0 && p.pair_sync != nullptr)
+      pair_epoch = ((unsigned)scalar_load_int(
+                        reinterpret_cast<const int *>(p.pair_sync), 0) &
+                    0x7fffffffu) + 1u;
+  }
   auto pair_rsrc = [&]() {
     return make_rsrc(reinterpret_cast<const char *>(p.pair_partials));
   };
@@ -854,7 +872,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (wave == kNW - 1 && lane == 0 && !p.pair_fault)
-        __hip_atomic_store(p.pair_flags + pair_id, p.pair_epoch,
+        __hip_atomic_store(p.pair_flags + pair_id, pair_epoch,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       tl(5);
       zero_acc();
@@ -873,7 +891,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         while (!(got = __hip_atomic_load(p.pair_flags + pair_id,
                                          __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT) ==
-                       p.pair_epoch) &&
+                       pair_epoch) &&
                __builtin_amdgcn_s_memrealtime() - t0 < kPairWaitTicks)
           __builtin_amdgcn_s_sleep(1);
         if (!got)
@@ -1911,6 +1929,23 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       break;
     }
   }  // tiles of a persistent workgroup
+  if constexpr (kPairs) {
+    if (p.pair != 0 && p.pair_sync != nullptr) {
+      // Captured launch: arrive; the last arriver advances the epoch word
+      // for the next replay and resets the count (GemmParams::pair_sync).
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned d = __hip_atomic_fetch_add(
+            p.pair_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d + 1 == gridDim.x) {
+          __hip_atomic_store(p.pair_sync + 1, 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.pair_sync, (pair_epoch & 0x7fffffffu),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
 #undef SEG_STAMP
 #undef SEG_ACCUM
 }

@@ -267,6 +267,10 @@ int sputnik_pair_errors(void) { return sputnik_amd::PairErrors(); }
 
 void sputnik_debug_pair_fault(int on) { sputnik_amd::SetPairFault(on); }
 
+int sputnik_capture_workspaces(void) {
+  return sputnik_amd::CaptureWorkspaces();
+}
+
 size_t sputnik_abi_block_matrix_size(void) { return sizeof(BlockMatrix); }
 
 size_t sputnik_abi_block_matrix_offset(int field) {

@@ -33,10 +33,11 @@ namespace sputnik_amd {
 // GemmParams::debug.
 static unsigned long long *g_debug = nullptr;
 
+constexpr int kMaxDevices = 64;
+
 // Compute units of a device, queried once per device (every SDD and every
 // pair-eligible DSD/DDS call needs it).
 static int DeviceCUs(int dev) {
-  constexpr int kMaxDevices = 64;
   static int cached[kMaxDevices] = {};
   if (dev < 0 || dev >= kMaxDevices) return 0;
   int cus = __atomic_load_n(&cached[dev], __ATOMIC_RELAXED);
@@ -57,19 +58,25 @@ static int DeviceCUs(int dev) {
 // Every launch carries a new epoch; a consumer waits for its own epoch, so a
 // flag left by an earlier launch (or by a producer that published after its
 // consumer gave up) can never satisfy a later launch, and nothing has to be
-// reset. A launch captured into a graph would replay one baked-in epoch
-// (and could replay on another stream), so pairs are off while capturing.
+// reset. A launch captured into a graph replays one set of arguments and
+// may replay on any stream, so captured launches get a workspace of their
+// own per (device, capture, capturing stream) and keep their epoch on the
+// device (GemmParams::pair_sync): replays of one graph are ordered behind
+// each other, and no eager launch or other capture shares that workspace.
 struct PairSlot {
   int device = -1;
   hipStream_t stream = nullptr;
+  unsigned long long capture = 0;  // capture id (capture table only)
   float *partials = nullptr;
-  unsigned *flags = nullptr;  // [pairs] flags, then the error word
+  unsigned *flags = nullptr;  // [pairs] flags, the error word, [epoch, count]
   unsigned epoch = 0;
   int pairs = 0;  // capacity
   int slots = 0;  // resident workgroups on the device
 };
 constexpr int kMaxPairSlots = 16;
+constexpr int kMaxCaptureSlots = 64;
 static PairSlot g_pairs[kMaxPairSlots];
+static PairSlot g_capture_pairs[kMaxCaptureSlots];
 static std::mutex g_pairs_mu;
 static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
 
@@ -82,20 +89,61 @@ static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
 struct CounterSlot {
   int device = -1;
   hipStream_t stream = nullptr;
+  unsigned long long capture = 0;  // capture id (capture table only)
   unsigned long long *counter = nullptr;  // [fetch, done]
 };
 static CounterSlot g_counters[kMaxPairSlots];
+static CounterSlot g_capture_counters[kMaxCaptureSlots];
+
+// Capture status of `stream`: 0 not capturing, 1 capturing (id in *id),
+// -1 the query failed or the capture is invalidated (no workspace then).
+static int CaptureState(hipStream_t stream, unsigned long long *id) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  *id = 0;
+  if (hipStreamGetCaptureInfo(stream, &cs, id) != hipSuccess) return -1;
+  if (cs == hipStreamCaptureStatusNone) return 0;
+  return cs == hipStreamCaptureStatusActive ? 1 : -1;
+}
+
+// Device memory for a workspace, zero-filled, callable while `stream` is
+// being captured: the thread switches to relaxed capture mode (hipMalloc is
+// not a stream operation), and the fill runs on a private non-blocking
+// stream that no capture touches, synchronized before returning.
+static hipError_t AllocZeroed(void **ptr, size_t bytes, int dev) {
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  static hipStream_t side[kMaxDevices] = {};
+  hipError_t e = hipSuccess;
+  if (dev < 0 || dev >= kMaxDevices) e = hipErrorInvalidDevice;
+  if (e == hipSuccess && side[dev] == nullptr)
+    e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
+  *ptr = nullptr;
+  if (e == hipSuccess) e = hipMalloc(ptr, bytes);
+  if (e == hipSuccess) e = hipMemsetAsync(*ptr, 0, bytes, side[dev]);
+  if (e == hipSuccess) e = hipStreamSynchronize(side[dev]);
+  if (e != hipSuccess && *ptr != nullptr) {
+    (void)hipFree(*ptr);
+    *ptr = nullptr;
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  return e;
+}
 
 // A (device, stream) table ran out of slots: the caller falls back to the
 // plain launch (correct, slower); said once per process.
-static void WarnSlotsFull(const char *what) {
-  static bool warned[2] = {false, false};
-  const int i = what[0] == 'p' ? 0 : 1;
-  if (!warned[i]) {
-    warned[i] = true;
-    SPUTNIK_LOG(WARNING) << "sputnik-amd: more than " << kMaxPairSlots
-                         << " streams use " << what
-                         << "; further streams run without it";
+// kind: 0 pair balancing, 1 persistent launches; +2 in captured graphs.
+static void WarnSlotsFull(int kind) {
+  static bool warned[4] = {false, false, false, false};
+  static const char *const what[4] = {
+      "streams use pair balancing", "streams use persistent launches",
+      "graph captures use pair balancing",
+      "graph captures use persistent launches"};
+  if (kind >= 0 && kind < 4 && !warned[kind]) {
+    warned[kind] = true;
+    SPUTNIK_LOG(WARNING) << "sputnik-amd: more than "
+                         << (kind < 2 ? kMaxPairSlots : kMaxCaptureSlots)
+                         << " " << what[kind]
+                         << "; further ones run without it";
   }
 }
 
@@ -129,51 +177,56 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
   if (stream == hipStreamPerThread) return;  // many streams, one handle
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
-      cs != hipStreamCaptureStatusNone)
-    return;
+  unsigned long long capture = 0;
+  const int capturing = CaptureState(stream, &capture);
+  if (capturing < 0) return;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
+  PairSlot *table = capturing ? g_capture_pairs : g_pairs;
+  const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   PairSlot *slot = nullptr;
-  for (auto &s : g_pairs)
-    if (s.partials != nullptr && s.device == dev && s.stream == stream) {
+  for (int i = 0; i < n_table; ++i) {
+    PairSlot &s = table[i];
+    if (s.partials != nullptr && s.device == dev && s.stream == stream &&
+        s.capture == capture) {
       slot = &s;
       break;
     }
+  }
   if (slot == nullptr) {
-    for (auto &s : g_pairs)
-      if (s.partials == nullptr) {
-        slot = &s;
+    for (int i = 0; i < n_table; ++i)
+      if (table[i].partials == nullptr) {
+        slot = &table[i];
         break;
       }
     if (slot == nullptr) {
-      WarnSlotsFull("pair balancing");
+      WarnSlotsFull(capturing ? 2 : 0);
       return;
     }
     const int cus = DeviceCUs(dev);
     if (cus <= 0) return;
     const int slots = cus * CfgSparse::kWGs;
     // Partial slots: slots / 2 pairs, or one per tile in split mode (at most
-    // slots / 2 tiles). 128 x 256 KiB = 32 MiB per stream on MI355X.
+    // slots / 2 tiles). 128 x 256 KiB = 32 MiB per workspace on MI355X.
     const int pairs = slots / 2;
-    float *partials = nullptr;
-    unsigned *flags = nullptr;
-    if (hipMalloc(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
-                                 sizeof(float)) != hipSuccess)
+    void *partials = nullptr, *flags = nullptr;
+    if (AllocZeroed(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
+                                   sizeof(float), dev) != hipSuccess)
       return;
-    const size_t flag_bytes = (pairs + 1) * sizeof(unsigned);
-    if (hipMalloc(&flags, flag_bytes) != hipSuccess ||
-        hipMemset(flags, 0, flag_bytes) != hipSuccess) {
+    if (AllocZeroed(&flags, (pairs + 3) * sizeof(unsigned), dev) !=
+        hipSuccess) {
+      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
       (void)hipFree(partials);
-      if (flags) (void)hipFree(flags);
+      (void)hipThreadExchangeStreamCaptureMode(&mode);
       return;
     }
     slot->device = dev;
     slot->stream = stream;
-    slot->partials = partials;
-    slot->flags = flags;
+    slot->capture = capture;
+    slot->partials = static_cast<float *>(partials);
+    slot->flags = static_cast<unsigned *>(flags);
     slot->pairs = pairs;
     slot->slots = slots;
   }
@@ -184,6 +237,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair_flags = slot->flags;
   p->pair_epoch = slot->epoch;
   p->pair_error = slot->flags + slot->pairs;
+  p->pair_sync = capturing ? slot->flags + slot->pairs + 1 : nullptr;
   p->pair_fault = g_pair_fault;
   // Two panels x half the pairs per XCD (GemmParams::pair_xcd2) from a mean
   // of 8 blocks per row: DSD 4096^3 A/B (r02m) 30% / 50% / 90% +1.2 / +2.7
@@ -241,7 +295,9 @@ int PairErrors() {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
   int total = 0;
-  for (auto &s : g_pairs) {
+  for (int i = 0; i < kMaxPairSlots + kMaxCaptureSlots; ++i) {
+    PairSlot &s = i < kMaxPairSlots ? g_pairs[i]
+                                    : g_capture_pairs[i - kMaxPairSlots];
     if (s.partials == nullptr || s.device != dev) continue;
     unsigned word = 0;
     if (hipMemcpy(&word, s.flags + s.pairs, sizeof(word),
@@ -259,6 +315,18 @@ int PairErrors() {
 }
 
 void SetPairFault(int on) { g_pair_fault = on != 0; }
+
+int CaptureWorkspaces() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  int n = 0;
+  for (const auto &s : g_capture_pairs)
+    n += s.partials != nullptr && s.device == dev;
+  for (const auto &c : g_capture_counters)
+    n += c.counter != nullptr && c.device == dev;
+  return n;
+}
 
 namespace {
 
@@ -628,36 +696,40 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   const int slots = cus * CfgTall::kWGs;
   if (!persistent || slots <= 0 || p->num_tiles <= slots) return true;
   if (stream == hipStreamPerThread) return true;  // many streams, one handle
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &cs) != hipSuccess ||
-      cs != hipStreamCaptureStatusNone)
-    return true;  // host-side counter base: not replayable
+  // A captured launch gets a counter pair of its own capture (the kernel
+  // leaves it at zero, so every replay starts clean).
+  unsigned long long capture = 0;
+  const int capturing = CaptureState(stream, &capture);
+  if (capturing < 0) return true;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
+  CounterSlot *table = capturing ? g_capture_counters : g_counters;
+  const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   CounterSlot *slot = nullptr;
-  for (auto &c : g_counters)
-    if (c.counter != nullptr && c.device == dev && c.stream == stream) {
+  for (int i = 0; i < n_table; ++i) {
+    CounterSlot &c = table[i];
+    if (c.counter != nullptr && c.device == dev && c.stream == stream &&
+        c.capture == capture) {
       slot = &c;
       break;
     }
+  }
   if (slot == nullptr) {
-    for (auto &c : g_counters)
-      if (c.counter == nullptr) {
-        slot = &c;
+    for (int i = 0; i < n_table; ++i)
+      if (table[i].counter == nullptr) {
+        slot = &table[i];
         break;
       }
     if (slot == nullptr) {
-      WarnSlotsFull("persistent launches");
+      WarnSlotsFull(capturing ? 3 : 1);
       return true;
     }
-    unsigned long long *ctr = nullptr;
-    if (hipMalloc(&ctr, 2 * sizeof(*ctr)) != hipSuccess) return true;
-    if (hipMemset(ctr, 0, 2 * sizeof(*ctr)) != hipSuccess) {
-      (void)hipFree(ctr);
+    void *ctr = nullptr;
+    if (AllocZeroed(&ctr, 2 * sizeof(unsigned long long), dev) != hipSuccess)
       return true;
-    }
     slot->device = dev;
     slot->stream = stream;
-    slot->counter = ctr;
+    slot->capture = capture;
+    slot->counter = static_cast<unsigned long long *>(ctr);
   }
   p->grid = slots;
   p->persistent = 1;

@@ -456,10 +456,11 @@ def test_tall_persistent_two_host_threads_one_stream():
 
 
 def test_graph_capture_with_pairs():
-    """A stream whose pair workspace already exists is captured into a
-    graph: pairs are off inside the capture, so replays (here on the
-    capturing stream and interleaved with eager calls that do use pairs)
-    stay exact."""
+    """A pair-balanced DSD captured into a graph gets a workspace of its own
+    capture with a device-side epoch (GemmParams::pair_sync): replays on the
+    capturing stream, on another stream, interleaved with eager pair
+    launches on the capturing stream (whose workspace already existed), all
+    stay bit-exact, and no hand-off times out."""
     got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
                                     "f16", seed=6)
     s = torch.cuda.Stream()
@@ -468,24 +469,60 @@ def test_graph_capture_with_pairs():
         sp.MatmulEx(A.m, False, Bd.m, False, C)  # creates s's workspace
     torch.cuda.current_stream().wait_stream(s)
     _equal(got, want, "eager on s")
+    before = sp.capture_workspaces()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         sp.MatmulEx(A.m, False, Bd.m, False, C)
-    for _ in range(3):
+    assert sp.capture_workspaces() == before + 1, "captured launch used pairs"
+    other = torch.cuda.Stream()
+    for i in range(4):
         got.fill_(float("nan"))
-        g.replay()
+        if i % 2:
+            other.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(other):
+                g.replay()
+            torch.cuda.current_stream().wait_stream(other)
+        else:
+            g.replay()
         _equal(got, want, "graph replay")
         got.fill_(float("nan"))
         sp.MatmulEx(A.m, False, Bd.m, False, C)
         _equal(got, want, "eager between replays")
+    # Back-to-back replays: each reads the epoch the previous one advanced.
+    for _ in range(8):
+        g.replay()
+    _equal(got, want, "back-to-back replays")
+    assert sp.pair_errors() == 0
+
+
+def test_graph_capture_split_and_dds():
+    """Split mode (a 512-row DSD panel) and a pair-balanced DDS captured in
+    one graph: two launches share the capture's workspace one after the
+    other; replays stay bit-exact."""
+    got1, want1, (A1, B1, C1) = kat_dsd(512, 4096, 4096, 0.5, False, False,
+                                        "f16", seed=7)
+    got2, want2, (A2, B2, C2) = kat_dds(4096, 4096, 4096, 0.5, False, False,
+                                        "f16", ex=True, seed=8, handles=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.MatmulEx(A1.m, False, B1.m, False, C1)
+        sp.MatmulEx(A2.m, False, B2.m, False, C2)
+    for _ in range(3):
+        got1.fill_(float("nan"))
+        got2.fill_(float("nan"))
+        g.replay()
+        _equal(got1, want1, "split replay")
+        _equal(got2, want2, "dds replay")
     assert sp.pair_errors() == 0
 
 
 def test_graph_capture_tall_persistent():
     """A tall DSD captured into a graph on a stream whose persistent tile
-    counter already exists: the captured launch runs one tile per workgroup
-    (persistence is off under capture), so replays interleaved with eager
-    persistent launches on the same stream all stay exact."""
+    counter already exists: the captured launch gets a counter pair of its
+    own capture (the kernel leaves it at zero), so replays interleaved with
+    eager persistent launches on the same stream all stay exact."""
     rng = np.random.default_rng(12)
     A = ISparse(65536, 256, 0.3, rng, "f16")
     Bd = IDense(256, 512, rng, "f16")
@@ -497,9 +534,11 @@ def test_graph_capture_tall_persistent():
         sp.MatmulEx(A.m, False, Bd.m, False, C)  # creates s's counter
     torch.cuda.current_stream().wait_stream(s)
     _equal(got, want, "eager on s")
+    before = sp.capture_workspaces()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         sp.MatmulEx(A.m, False, Bd.m, False, C)
+    assert sp.capture_workspaces() == before + 1, "captured launch persistent"
     for _ in range(3):
         got.fill_(float("nan"))
         g.replay()
