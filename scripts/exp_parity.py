@@ -42,11 +42,11 @@ def main():
         finite = bool(torch.isfinite(outs[0].float()).all())
         bad += sum(not v for v in res.values()) + (not finite)
         print(json.dumps({"case": f"{op} {tr} {dens}", "finite": finite, "equal": res}), flush=True)
-    # split mode: a few-row DSD panel
+    # split mode (few-row panels) and persistent tall launches
     import numpy as np
     from sputnik_amd import matrix_utils as mu
-    for m in (512, 1024):
-        nz = mu.nonzeros_for_density(m, 4096, 0.5)
+    for m, dens in ((512, 0.5), (1024, 0.5), (65536, 0.02), (32768, 0.3)):
+        nz = mu.nonzeros_for_density(m, 4096, dens)
         off, idx = mu.random_topology(m // 128, 32, nz // (128 * 128), np.random.default_rng(3))
         prob = bench.DsdProblem(m, 4096, off, idx, 4096, False, False, "f16", 0, dev)
         outs = []
@@ -59,7 +59,7 @@ def main():
             outs.append(prob.c_vals.clone())
         res = {os.path.basename(p): bool(torch.equal(o, outs[0])) for p, o in zip(libs[1:], outs[1:])}
         bad += sum(not v for v in res.values())
-        print(json.dumps({"case": f"split dsd M={m}", "equal": res}), flush=True)
+        print(json.dumps({"case": f"dsd M={m} {dens}", "equal": res}), flush=True)
     print(json.dumps({"mismatches": bad}))
     return 1 if bad else 0
 
