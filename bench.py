@@ -257,6 +257,7 @@ def dsd_panel(args, world, rank, device, density, m_total=None, seed_off=0):
     prob = DsdProblem((r1 - r0) * BLOCK, args.k, po, pi, args.n, False, False,
                       args.dtype, args.seed * 7919 + rank, device)
     prob.panel = (r0, r1)
+    prob.all_panels = mu.shard_rows_by_nnz(off, world)
     prob.total_nb = int(off[-1])
     return prob
 
@@ -751,24 +752,24 @@ def run_other(args, world, rank, device, build):
             extra["dense_anchor"] = anchor
     if args.workload == "panel" and world > 1:
         # Optional gather of the dense result (config 5): reported beside the
-        # hot path, never inside it. Equal-size panels of the padded maximum.
+        # hot path, never inside it. The library's gather_row_panels
+        # (sputnik_amd/gather.py): the nnz-balanced panels differ in rows, so
+        # it runs one grouped send/recv set (RCCL over xGMI), no padding.
         import torch
-        import torch.distributed as dist
-        rows = torch.tensor([prob.C.rows], device=device)
-        dist.all_reduce(rows, op=dist.ReduceOp.MAX)
-        pad = torch.zeros(int(rows.item()) * args.n, dtype=prob.c_vals.dtype,
-                          device=device)
-        pad[:prob.c_vals.numel()] = prob.c_vals
-        full = torch.empty(world * pad.numel(), dtype=pad.dtype, device=device)
-        dist.all_gather_into_tensor(full, pad)
+        import sputnik_amd as sp
+        panels = [tuple(int(x) for x in pr) for pr in prob.all_panels]
+        c_panel = prob.c_vals.view(prob.C.rows, args.n)
+        full = sp.gather_row_panels(c_panel, panels)
         torch.cuda.synchronize()
         barrier(world)
         t0 = time.perf_counter()
         for _ in range(5):
-            dist.all_gather_into_tensor(full, pad)
+            sp.gather_row_panels(c_panel, panels, out=full)
         torch.cuda.synchronize()
         ag = max_over_ranks((time.perf_counter() - t0) / 5 * 1e3, world)
         extra["allgather_ms"] = round(ag, 4)
+        extra["allgather_method"] = ("all_gather_into_tensor" if len(
+            {p1 - p0 for p0, p1 in panels}) == 1 else "batch_isend_irecv")
         extra["allgather_GBps_per_rank"] = round(
             full.numel() * full.element_size() * (world - 1) / world / (ag * 1e-3) / 1e9, 1)
         del full

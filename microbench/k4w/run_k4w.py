@@ -1,0 +1,124 @@
+"""Experiment driver: the 4-wave hand-scheduled DSD kernel (k4w.hip) against
+the shipped kernel, same data, one process, interleaved timing.
+
+python microbench/k4w/run_k4w.py [--build-only] [--density 0.5] [--uniform]
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+SO = os.path.join(HERE, "libk4w.so")
+
+
+def build():
+    subprocess.run([sys.executable, os.path.join(HERE, "gen_k4w.py"),
+                    os.path.join(HERE, "k4w_loop.inc")], check=True)
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-shared",
+                    "--offload-arch=gfx950", "-save-temps=obj",
+                    os.path.join(HERE, "k4w.hip"), "-o", SO], check=True, cwd=HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build-only", action="store_true")
+    ap.add_argument("--density", type=float, default=0.5)
+    ap.add_argument("--uniform", action="store_true",
+                    help="every block-row holds the same number of blocks")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--calls", type=int, default=50)
+    ap.add_argument("--dtype", default="f16")
+    a = ap.parse_args()
+    if a.build_only:
+        build()
+        return
+    import numpy as np
+    import torch
+    import bench
+    from sputnik_amd import matrix_utils as mu
+
+    dev = torch.device("cuda:0")
+    d = 4096
+    R = d // 128
+    rng = np.random.default_rng(1)
+    if a.uniform:
+        per = int(round(R * a.density))
+        off = np.arange(R + 1, dtype=np.int32) * per
+        idx = np.concatenate([np.sort(rng.choice(R, per, replace=False))
+                              for _ in range(R)]).astype(np.int32)
+    else:
+        nz = mu.nonzeros_for_density(d, d, a.density)
+        off, idx = mu.random_topology(R, R, nz // (128 * 128), rng)
+    prob = bench.DsdProblem(d, d, off, idx, d, False, False, a.dtype, 7, dev)
+    ship = prob.launcher()
+    lib = ctypes.CDLL(SO)
+    offs_t = torch.from_numpy(np.asarray(off, np.int32)).to(dev)
+    idx_t = torch.from_numpy(np.asarray(idx).astype(np.int16)).to(dev)
+    c2 = torch.empty_like(prob.c_vals)
+    stream = torch.cuda.current_stream().cuda_stream
+    bf = 1 if a.dtype == "bf16" else 0
+
+    def mine():
+        return lib.k4w_dsd(ctypes.c_void_p(prob.a_vals.data_ptr()),
+                           ctypes.c_void_p(offs_t.data_ptr()),
+                           ctypes.c_void_p(idx_t.data_ptr()),
+                           ctypes.c_void_p(prob.b_vals.data_ptr()),
+                           ctypes.c_void_p(c2.data_ptr()), d, d, d, bf,
+                           ctypes.c_void_p(stream))
+
+    ship()
+    rc = mine()
+    torch.cuda.synchronize()
+    c1 = prob.c_vals.float().view(d, d)
+    cm = c2.float().view(d, d)
+    diff = (c1 - cm).abs()
+    res = {"rc": rc, "max_abs_diff_vs_shipped": float(diff.max()),
+           "rows_differing": int((diff.amax(1) > 0).sum()),
+           "nan": bool(torch.isnan(cm).any())}
+    # independent check: a few block-rows against fp32 torch
+    A = torch.zeros(d, d, device=dev)
+    av = prob.a_vals.float().view(-1, 128, 128)
+    rows = np.repeat(np.arange(R), np.diff(off))
+    for b in range(len(idx)):
+        r, c = int(rows[b]), int(idx[b])
+        A[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128] = av[b]
+    ref = A @ prob.b_vals.float().view(d, d)
+    err = ((cm - ref).abs() / (ref.abs() + ref.pow(2).mean().sqrt())).max()
+    res["max_rel_err_vs_fp32"] = float(err)
+    print(json.dumps(res), flush=True)
+
+    def timed(fn, calls):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(calls):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) * 1e3 / calls
+
+    for _ in range(200):
+        ship()
+        mine()
+    torch.cuda.synchronize()
+    ts, tm = [], []
+    for _ in range(a.rounds):
+        ts.append(timed(ship, a.calls))
+        tm.append(timed(mine, a.calls))
+    flops = prob.flops
+    out = {"density": a.density, "uniform": a.uniform, "dtype": a.dtype,
+           "shipped_us": sorted(ts)[len(ts) // 2], "k4w_us": sorted(tm)[len(tm) // 2],
+           "shipped_all": [round(x, 2) for x in ts], "k4w_all": [round(x, 2) for x in tm]}
+    out["shipped_tflops"] = round(flops / out["shipped_us"] / 1e6, 1)
+    out["k4w_tflops"] = round(flops / out["k4w_us"] / 1e6, 1)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

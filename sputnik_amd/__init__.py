@@ -417,6 +417,12 @@ def version() -> str:
     return lib().sputnik_version().decode()
 
 
+# Full-result gathers of a sharded product (host-side torch.distributed, off
+# the hot path; sputnik_amd/gather.py).
+from .gather import (allgather_concat, gather_block_runs,  # noqa: E402
+                     gather_col_panels, gather_row_panels)
+
+
 __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
@@ -425,4 +431,6 @@ __all__ = [
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",
     "SputnikError", "Transpose", "can_implement", "lib", "version",
+    "allgather_concat", "gather_row_panels", "gather_col_panels",
+    "gather_block_runs",
 ]

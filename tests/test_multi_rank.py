@@ -248,7 +248,11 @@ def _worker_hip(rank, world, port, out_path):
     p_off, p_idx, p_vals = mu.slice_block_rows(off, idx, vals, r0, r1)
     panel = (_hip_dsd(p_off, p_idx, p_vals, r1 - r0, C, b) if r1 > r0
              else np.zeros((0, N), np.float32))
-    full = np.concatenate(_gather_equal(panel, world))
+    # The library's gather (sputnik_amd.gather_row_panels) on the host copies
+    # of the HIP panels (gloo carries CPU tensors).
+    import sputnik_amd as sp
+    full = sp.gather_row_panels(torch.from_numpy(panel),
+                                mu.shard_rows_by_nnz(off, world)).numpy()
     if rank == 0:
         np.save(out_path, full)
     dist.destroy_process_group()
@@ -300,3 +304,98 @@ def test_bench_two_ranks_shard_one_matrix(scaling):
     nb0 = line["by_density"]["0.5"]["nnz_blocks_per_rank"]
     total = (m // 128) * 32 // 2
     assert abs(nb0 - total / 2) <= 32, (nb0, total)
+
+
+# ---- the library's full-result gathers (sputnik_amd/gather.py) --------------
+
+def _worker_gather(rank, world, port, out_path, method):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sputnik_amd as sp
+    from oracle import oracle as O
+    # DSD row panels: nonzero-balanced, so the row counts differ per rank
+    R, C, N, off, idx, vals, b = _problem()
+    panels = mu.shard_rows_by_nnz(off, world)
+    r0, r1 = panels[rank]
+    p_off, p_idx, p_vals = mu.slice_block_rows(off, idx, vals, r0, r1)
+    rows = (r1 - r0) * 128
+    panel = np.zeros((rows, N), np.float32)
+    if rows:
+        panel = O.gemm(mu.to_dense(rows, C * 128, p_off, p_idx, p_vals), False,
+                       b, False, a_mask=mu.block_mask(p_off, p_idx, C))
+    dsd = sp.gather_row_panels(torch.from_numpy(panel), panels, method=method)
+    # DDS column panels
+    M, KB, NB, off2, idx2, vals2, a = _pair_problem()
+    cpan = mu.shard_cols_by_nnz(off2, idx2, NB, world)
+    c0, c1 = cpan[rank]
+    q_off, q_idx, q_vals = mu.slice_block_cols(off2, idx2, vals2, c0, c1)
+    cols = (c1 - c0) * 128
+    cp = np.zeros((M, cols), np.float32)
+    if cols:
+        cp = O.gemm(a, False, mu.to_dense(KB * 128, cols, q_off, q_idx, q_vals),
+                    False, b_mask=mu.block_mask(q_off, q_idx, c1 - c0))
+    dds = sp.gather_col_panels(torch.from_numpy(np.ascontiguousarray(cp)), cpan,
+                               method=method)
+    # SDD block runs (values stand in for computed blocks: the gather is what
+    # is under test)
+    runs = mu.shard_blocks(len(idx2), world)
+    b0, b1 = runs[rank]
+    sdd = sp.gather_block_runs(torch.from_numpy(vals2[b0:b1].reshape(-1)), runs,
+                               method=method)
+    if rank == 0:
+        np.savez(out_path, dsd=dsd.numpy(), dds=dds.numpy(), sdd=sdd.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,method", [(2, "auto"), (2, "padded"),
+                                          (3, "auto"), (3, "p2p")])
+def test_gather_panels_match_unsharded(tmp_path, world, method):
+    from oracle import oracle as O
+    out = str(tmp_path / "g.npz")
+    mp.spawn(_worker_gather, args=(world, _free_port(), out, method),
+             nprocs=world, join=True)
+    got = np.load(out)
+    R, C, N, off, idx, vals, b = _problem()
+    assert np.array_equal(got["dsd"], O.gemm(
+        mu.to_dense(R * 128, C * 128, off, idx, vals), False, b, False))
+    M, KB, NB, off2, idx2, vals2, a = _pair_problem()
+    assert np.array_equal(got["dds"], O.gemm(
+        a, False, mu.to_dense(KB * 128, NB * 128, off2, idx2, vals2), False))
+    assert np.array_equal(got["sdd"], vals2)
+
+
+def test_gather_checks_cover():
+    from sputnik_amd import gather
+    with pytest.raises(ValueError):
+        gather._check_cover([(0, 2), (3, 4)])
+    with pytest.raises(ValueError):
+        gather._check_cover([(1, 2)])
+    gather._check_cover([(0, 0), (0, 5), (5, 5)])
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_panel_gather():
+    """bench.py --workload panel at world size 2 (gloo, both ranks on the
+    box's device): the rank panels of config 5 and the timed full-result
+    gather (sputnik_amd.gather_row_panels) beside the hot path."""
+    import json
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--no-cpu",
+           "--dist-backend", "gloo", "--workload", "panel"]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                         cwd=root)
+    assert res.returncode == 0, res.stderr[-2000:]
+    line = json.loads([x for x in res.stdout.splitlines()
+                       if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert line["allgather_ms"] > 0
+    assert line["allgather_method"] in ("all_gather_into_tensor",
+                                        "batch_isend_irecv")
