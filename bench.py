@@ -72,8 +72,8 @@ def parse():
                          "op: one product/transpose; transpose: metadata")
     ap.add_argument("--graph", action="store_true",
                     help="time replays of a hipGraph captured around one step "
-                         "(captured launches run without pair hand-offs and "
-                         "persistent tile fetch: dispatch.cpp)")
+                         "(captured launches use a pair workspace and tile "
+                         "counter of their own capture: INTEGRATION §3b)")
     ap.add_argument("--sweep-ops", default="dsd,dds,sdd")
     ap.add_argument("--sweep-dims", default="512,1024,2048,4096,8192,16384")
     ap.add_argument("--sweep-densities", default="1.0,0.5,0.1,0.01")

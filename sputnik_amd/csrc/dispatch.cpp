@@ -17,6 +17,7 @@
 //   SDD  C = op(A) op(B):  S = op(A) (dense),  D = op(B), O = C's blocks.
 // A sparse S read in column order (DSD TN/TT, DDS NN/TN) uses the transposed
 // metadata (offsets_t, indices_t, block_offsets), exactly like the reference.
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <mutex>
@@ -67,6 +68,10 @@ struct PairSlot {
   int device = -1;
   hipStream_t stream = nullptr;
   unsigned long long capture = 0;  // capture id (capture table only)
+  // Capture table only: set (by a user-object destructor on HIP's callback
+  // thread) once the captured graph and every executable made from it are
+  // destroyed; ReclaimCaptureSlots then frees the memory.
+  std::atomic<int> released{0};
   float *partials = nullptr;
   unsigned *flags = nullptr;  // [pairs] flags, the error word, [epoch, count]
   unsigned epoch = 0;
@@ -90,6 +95,7 @@ struct CounterSlot {
   int device = -1;
   hipStream_t stream = nullptr;
   unsigned long long capture = 0;  // capture id (capture table only)
+  std::atomic<int> released{0};  // as PairSlot::released
   unsigned long long *counter = nullptr;  // [fetch, done]
 };
 static CounterSlot g_counters[kMaxPairSlots];
@@ -128,6 +134,51 @@ static hipError_t AllocZeroed(void **ptr, size_t bytes, int dev) {
   (void)hipThreadExchangeStreamCaptureMode(&mode);
   return e;
 }
+
+// Ties a capture-table slot to the lifetime of the graph being captured on
+// `stream`: a user object retained by the graph (executables instantiated
+// from it retain it too) sets *released when the last reference goes, i.e.
+// once the graph and all its executables are destroyed and no launch of them
+// is pending. A destructor may not call HIP, so the memory is freed later by
+// ReclaimCaptureSlots. Returns false if the graph cannot be tied (the slot
+// then lives for the process, as before).
+static void MarkReleased(void *flag) {
+  static_cast<std::atomic<int> *>(flag)->store(1, std::memory_order_release);
+}
+static bool TieToCapturedGraph(hipStream_t stream, std::atomic<int> *released) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t graph = nullptr;
+  const hipGraphNode_t *deps = nullptr;
+  size_t ndeps = 0;
+  if (hipStreamGetCaptureInfo_v2(stream, &cs, &id, &graph, &deps, &ndeps) !=
+          hipSuccess ||
+      cs != hipStreamCaptureStatusActive || graph == nullptr)
+    return false;
+  hipUserObject_t obj = nullptr;
+  if (hipUserObjectCreate(&obj, released, MarkReleased, 1,
+                          hipUserObjectNoDestructorSync) != hipSuccess)
+    return false;
+  // Move our one reference into the graph: the graph now owns the object.
+  if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) !=
+      hipSuccess) {
+    (void)hipUserObjectRelease(obj, 1);
+    return false;
+  }
+  return true;
+}
+
+// Frees the capture-table workspaces whose graphs are gone (caller holds
+// g_pairs_mu; called from eager launches only, never while this thread's
+// stream is being captured, since hipFree is not a capturable call).
+static void FreeQuiet(void *ptr) {
+  if (ptr == nullptr) return;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  (void)hipFree(ptr);
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+}
+static void ReclaimCaptureSlots();
 
 // A (device, stream) table ran out of slots: the caller falls back to the
 // plain launch (correct, slower); said once per process.
@@ -183,6 +234,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
+  if (!capturing) ReclaimCaptureSlots();
   PairSlot *table = capturing ? g_capture_pairs : g_pairs;
   const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   PairSlot *slot = nullptr;
@@ -229,6 +281,8 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     slot->flags = static_cast<unsigned *>(flags);
     slot->pairs = pairs;
     slot->slots = slots;
+    slot->released.store(0, std::memory_order_relaxed);
+    if (capturing) (void)TieToCapturedGraph(stream, &slot->released);
   }
   if (p->num_tiles > slot->slots) return;
   if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
@@ -271,9 +325,13 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
       if (tiles * 2 > slot->slots) break;
       bn = cand;
     }
-    static const int max_narrow = [] {  // tuning: 512 keeps the wide tile
+    // Tuning floor of the tile width: 512 keeps the wide tile. Only the
+    // three instantiated widths are valid (Launch has split kernels for 128,
+    // 256 and 512 columns); anything else is rounded up to the next one.
+    static const int max_narrow = [] {
       const char *e = std::getenv("SPUTNIK_AMD_SPLIT_MIN_BN");
-      return e != nullptr ? std::atoi(e) : 128;
+      const int v = e != nullptr ? std::atoi(e) : 128;
+      return v <= 128 ? 128 : v <= 256 ? 256 : CfgSparse::kBN;
     }();
     if (bn < max_narrow) bn = max_narrow;
     p->split_bn = bn;
@@ -316,10 +374,39 @@ int PairErrors() {
 
 void SetPairFault(int on) { g_pair_fault = on != 0; }
 
+static void ReclaimCaptureSlots() {
+  for (auto &sl : g_capture_pairs) {
+    if (sl.partials == nullptr ||
+        sl.released.load(std::memory_order_acquire) == 0)
+      continue;
+    FreeQuiet(sl.partials);
+    FreeQuiet(sl.flags);
+    sl.partials = nullptr;
+    sl.flags = nullptr;
+    sl.device = -1;
+    sl.stream = nullptr;
+    sl.capture = 0;
+    sl.epoch = 0;
+    sl.pairs = sl.slots = 0;
+    sl.released.store(0, std::memory_order_relaxed);
+  }
+  for (auto &c : g_capture_counters) {
+    if (c.counter == nullptr || c.released.load(std::memory_order_acquire) == 0)
+      continue;
+    FreeQuiet(c.counter);
+    c.counter = nullptr;
+    c.device = -1;
+    c.stream = nullptr;
+    c.capture = 0;
+    c.released.store(0, std::memory_order_relaxed);
+  }
+}
+
 int CaptureWorkspaces() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -1;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
+  ReclaimCaptureSlots();
   int n = 0;
   for (const auto &s : g_capture_pairs)
     n += s.partials != nullptr && s.device == dev;
@@ -675,7 +762,12 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   }();
   if (mode == 0) return false;
   if (mode == 2) {
+    // Forced tall (experiments): drop every pair-launch setting PreparePairs
+    // made, split mode's grid and tile width included.
     p->pair = 0;
+    p->pair_split = 1;
+    p->split_bn = 0;
+    p->grid = 0;
   } else if (p->num_rows <= kLptRows || p->pair != 0) {
     return false;
   }
@@ -702,6 +794,7 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   const int capturing = CaptureState(stream, &capture);
   if (capturing < 0) return true;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
+  if (!capturing) ReclaimCaptureSlots();
   CounterSlot *table = capturing ? g_capture_counters : g_counters;
   const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   CounterSlot *slot = nullptr;
@@ -730,6 +823,8 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
     slot->stream = stream;
     slot->capture = capture;
     slot->counter = static_cast<unsigned long long *>(ctr);
+    slot->released.store(0, std::memory_order_relaxed);
+    if (capturing) (void)TieToCapturedGraph(stream, &slot->released);
   }
   p->grid = slots;
   p->persistent = 1;

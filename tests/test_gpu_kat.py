@@ -495,6 +495,46 @@ def test_graph_capture_with_pairs():
     assert sp.pair_errors() == 0
 
 
+def test_graph_capture_workspace_freed_with_graph():
+    """A capture's pair workspace (32 MiB) and persistent counter live as long
+    as the captured graph: destroying the graph and its executable releases
+    them (a user object retained by the graph, dispatch.cpp
+    TieToCapturedGraph), so re-capturing per shape does not pin memory or
+    fill the capture tables."""
+    import time
+    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
+                                    "f16", seed=9)
+    rng = np.random.default_rng(14)
+    T = ISparse(65536, 256, 0.3, rng, "f16")
+    Td = IDense(256, 512, rng, "f16")
+    CT, gotT = _nan_out(65536, 512, "f16")
+    torch.cuda.synchronize()
+    base = sp.capture_workspaces()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    for rep in range(3):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            sp.MatmulEx(A.m, False, Bd.m, False, C)
+            sp.MatmulEx(T.m, False, Td.m, False, CT)
+        assert sp.capture_workspaces() == base + 2, "pairs + tall counter"
+        got.fill_(float("nan"))
+        g.replay()
+        _equal(got, want, f"replay {rep}")
+        torch.cuda.synchronize()
+        g.reset()
+        del g
+        torch.cuda.synchronize()
+        n = sp.capture_workspaces()
+        for _ in range(50):  # the destructor runs on HIP's callback thread
+            if n == base:
+                break
+            time.sleep(0.02)
+            n = sp.capture_workspaces()
+        assert n == base, f"capture workspaces still held: {n} vs {base}"
+    assert sp.pair_errors() == 0
+
+
 def test_graph_capture_split_and_dds():
     """Split mode (a 512-row DSD panel) and a pair-balanced DDS captured in
     one graph: two launches share the capture's workspace one after the
