@@ -137,6 +137,59 @@ def test_moe_config4_bf16_sampled():
                        f"moe dsd row-block {r}")
 
 
+def test_moe_config4_backward_bf16_sampled():
+    """The MegaBlocks backward of config 4's second layer at full size (8
+    experts, 8192 tokens, d_model 4096, d_ff 14336, bf16):
+      dW2 = h^T . dy   (DSD TN: h^T has 896 block-rows, the tall path, with
+                        h's transposed metadata built on the device),
+      dh  = dy . W2^T  at h's blocks (SDD NT).
+    Sampled row-blocks / blocks against the oracle."""
+    E, T, DM, FF = 8, 8192, 4096, 14336
+    cols = E * FF
+    rpe, cpe = T // E // 128, FF // 128
+    off, idx = mu.expert_block_diagonal(E, rpe, cpe)
+    nb = int(off[-1])
+    g = torch.Generator(device="cuda")
+    g.manual_seed(44)
+    rnd = lambda *s: (torch.rand(*s, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
+    hv, dy, w2 = rnd(nb, 128, 128), rnd(T, DM), rnd(cols, DM)
+    mk = lambda vals: sp.BlockMatrix(T, cols, 128, nb * 16384, vals,
+                                     torch.from_numpy(off).cuda(),
+                                     torch.from_numpy(idx.astype(np.int16)).cuda())
+    Hm = mk(hv)
+    sp.AllocateTransposeBuffers(Hm)
+    dw2 = torch.full((cols, DM), float("nan"), dtype=torch.bfloat16, device="cuda")
+    sp.Matmul(Hm, True, sp.Matrix(T, DM, dy), False, sp.Matrix(cols, DM, dw2))
+    dhv = torch.full((nb, 128, 128), float("nan"), dtype=torch.bfloat16,
+                     device="cuda")
+    dHm = mk(dhv)
+    sp.AllocateRowIndicesBuffer(dHm)
+    sp.RowIndices(dHm, dHm.row_indices)
+    sp.Matmul(sp.Matrix(T, DM, dy), False, sp.Matrix(cols, DM, w2), True, dHm)
+    _sync()
+    f = lambda t: t.float().cpu().numpy()
+    # dW2 row-block c (= h's block-column c, expert e = c // cpe): only the
+    # expert's tokens hold h blocks in that column.
+    rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
+    for c in (0, 111, 500, cols // 128 - 1):
+        e = c // cpe
+        t0, t1 = e * rpe * 128, (e + 1) * rpe * 128
+        hcol = np.concatenate([f(hv[b]) for b in range(nb)
+                               if idx[b] == c and t0 <= rows[b] * 128 < t1])
+        assert hcol.shape == (t1 - t0, 128)
+        ref = O.gemm(hcol.T.copy(), False, f(dy[t0:t1]), False,
+                     threads=H.oracle_threads())
+        H.assert_close(f(dw2[c * 128:(c + 1) * 128]), ref, "bf16",
+                       f"moe bwd dW2 row-block {c}")
+    for b in (0, 777, nb // 2 + 5, nb - 1):
+        r, c = int(rows[b]), int(idx[b])
+        ref = O.gemm(f(dy[r * 128:(r + 1) * 128]), False,
+                     f(w2[c * 128:(c + 1) * 128]).T.copy(), False,
+                     threads=H.oracle_threads())
+        H.assert_close(f(dhv[b]), ref, "bf16", f"moe bwd dh block {b}")
+    assert not torch.isnan(dw2.float()).any()
+
+
 def test_tall_panel_config5_sampled():
     """BASELINE config 5 at full size on one device: DSD M=131072, K=N=4096,
     2% density (656 blocks over 1024 block-rows, most rows empty). Empty

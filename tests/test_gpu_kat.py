@@ -130,11 +130,13 @@ def test_kat_dsd(ta, tb, dtype, k):
 
 
 @pytest.mark.parametrize("ta,tb", TRANSPOSES)
-def test_kat_dsd_ex_tall(ta, tb):
+@pytest.mark.parametrize("dtype,k", [("f16", 384), ("bf16", 256)])
+def test_kat_dsd_ex_tall(ta, tb, dtype, k):
     """> 256 block-rows (tall tile config), MatmulEx with precomputed
-    metadata, partial N tile."""
-    got, want, _ = kat_dsd(300 * 128, 384, 264, 0.3, ta, tb, "f16", ex=True)
-    _equal(got, want, f"dsd tall {ta}{tb}")
+    metadata, partial N tile; bf16 with K <= 256 stays exact (the MoE
+    backward's tall transposed products)."""
+    got, want, _ = kat_dsd(300 * 128, k, 264, 0.3, ta, tb, dtype, ex=True)
+    _equal(got, want, f"dsd tall {ta}{tb} {dtype}")
 
 
 def test_kat_tall_persistent_repeated():
@@ -251,9 +253,10 @@ def test_kat_dds(ta, tb, dtype, k):
 
 
 @pytest.mark.parametrize("ta,tb", TRANSPOSES)
-def test_kat_dds_ex_tall(ta, tb):
-    got, want = kat_dds(264, 384, 300 * 128, 0.3, ta, tb, "f16", ex=True)
-    _equal(got, want, f"dds tall {ta}{tb}")
+@pytest.mark.parametrize("dtype,k", [("f16", 384), ("bf16", 256)])
+def test_kat_dds_ex_tall(ta, tb, dtype, k):
+    got, want = kat_dds(264, k, 300 * 128, 0.3, ta, tb, dtype, ex=True)
+    _equal(got, want, f"dds tall {ta}{tb} {dtype}")
 
 
 def test_kat_dds_4096_pairs():
