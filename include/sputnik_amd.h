@@ -171,10 +171,18 @@ int sputnik_pair_errors(void);
 void sputnik_debug_pair_fault(int on);
 /* Workspaces made for launches captured into graphs on the current device
  * (pair-balancing workspaces + persistent tile counters). A captured launch
- * gets one per (capture, capturing stream), kept for the process's life; a
- * graph therefore must not be replayed concurrently with a second
- * instantiation of the same capture. Host-only query. */
+ * gets one per (capture, capturing stream); it is freed once the captured
+ * graph and every executable made from it are destroyed (the count drops at
+ * the next eager launch or query). A graph must not be replayed
+ * concurrently with a second instantiation of the same capture. Host-only
+ * query. */
 int sputnik_capture_workspaces(void);
+/* DSD NN kernel choice (tests and same-process A/B): 1 = the 4-wave
+ * hand-scheduled kernel where it applies and pays (the default; environment
+ * SPUTNIK_AMD_DSD4W=0 turns it off), 2 = wherever it applies, whatever the
+ * density, 0 = the 8-wave kernel everywhere, -1 = query only. Returns the
+ * previous choice. Process-wide. */
+int sputnik_select_dsd_kernel(int four_wave);
 
 #ifdef __cplusplus
 }  /* extern "C" */

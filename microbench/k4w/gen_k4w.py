@@ -31,12 +31,6 @@ def mfma(dt, m, n, s):
             f"v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], a[{a}:{a + 3}]")
 
 
-def zero_mfma(dt, m, n, s):
-    a = 4 * (8 * m + n)
-    return (f"v_mfma_f32_16x16x32_{dt} a[{a}:{a + 3}], v[{FD[s] + 4 * n}:{FD[s] + 4 * n + 3}], "
-            f"v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], 0")
-
-
 def d_reads(slot, s):
     out = []
     for n in range(8):
@@ -87,8 +81,26 @@ IDX_LOAD = ["s_min_u32 s78, s56, s74", "s_add_u32 s56, s56, 1",
 
 DMA_POS = [3, 9, 15, 21, 27, 33, 39, 45, 51, 57]
 
+# Experiment variants (ablations / placements); 0 is the kernel.
+VARIANTS = {
+    0: {},
+    1: {"no_dma": True},
+    2: {"no_reads": True},
+    3: {"no_dma": True, "no_reads": True, "no_barrier": True},
+    4: {"dma_pos": list(range(30, 50, 2))},
+    5: {"barrier_at": 40, "s_reads_at": 41},
+    6: {"dma_pos": [3, 7, 11, 15, 19, 23, 27, 31, 35, 39]},
+    7: {"no_barrier": True},
+    8: {"no_d_reads": True},
+    9: {"no_s_reads": True},
+    10: {"no_s_dma": True},
+    11: {"no_d_dma": True},
+    12: {"no_vmcnt": True},
+    13: {"no_lgkm": True},
+}
 
-def step(dt, H, first=False):
+
+def step(dt, H, opt):
     """Loop step H of a block: MFMAs on set H%2, reads of step i+1 from slot
     (H+1)%4 into the other set, DMA of step i+3 into slot (H+3)%4."""
     cur = H % 2
@@ -96,26 +108,33 @@ def step(dt, H, first=False):
     gaps = [[] for _ in range(64)]
     if H == 0:
         gaps[0] += IDX_LOAD
-    gaps[1].append("s_waitcnt vmcnt(10)")
+    if not opt.get("no_vmcnt"):
+        gaps[1].append("s_waitcnt vmcnt(10)")
     if H == 1:
         gaps[1] += SWITCH
-    dr = d_reads((H + 1) % 4, nxt)
-    for i, ins in enumerate(dr):
-        gaps[2 + i].append(ins)
-    gaps[18].append("s_barrier")
-    sr = s_reads((H + 1) % 4, nxt)
-    for i, ins in enumerate(sr):
-        gaps[19 + i].append(ins)
-    for (m0, ld), k in zip(dmas((H + 3) % 4), DMA_POS):
+    if not opt.get("no_reads") and not opt.get("no_d_reads"):
+        dr = d_reads((H + 1) % 4, nxt)
+        for i, ins in enumerate(dr):
+            gaps[2 + i].append(ins)
+    if not opt.get("no_barrier"):
+        gaps[opt.get("barrier_at", 18)].append("s_barrier")
+    if not opt.get("no_reads") and not opt.get("no_s_reads"):
+        sr = s_reads((H + 1) % 4, nxt)
+        for i, ins in enumerate(sr):
+            gaps[opt.get("s_reads_at", 19) + i].append(ins)
+    for j, ((m0, ld), k) in enumerate(zip(dmas((H + 3) % 4), opt.get("dma_pos", DMA_POS))):
         gaps[k - 1].append(m0)
-        gaps[k].append(ld)
+        skip = (opt.get("no_dma") or (opt.get("no_s_dma") and j < 2)
+                or (opt.get("no_d_dma") and j >= 2))
+        if not skip:
+            gaps[k].append(ld)
     gaps[58] += ADVANCE if H != 0 else []
-    gaps[63].append("s_waitcnt lgkmcnt(0)")
+    gaps[63].append("s_waitcnt lgkmcnt(0)" if not opt.get("no_lgkm") else "s_nop 0")
     out = []
     idx = 0
     for m in range(8):
         for n in range(8):
-            out.append(zero_mfma(dt, m, n, cur) if first else mfma(dt, m, n, cur))
+            out.append(mfma(dt, m, n, cur))
             out += gaps[idx]
             idx += 1
     return out
@@ -173,11 +192,11 @@ def epilogue():
     return out
 
 
-def build(dt):
+def build(dt, opt):
     body = prologue()
     body.append("L_loop_%=:")
     for H in range(4):
-        body += step(dt, H)
+        body += step(dt, H, opt)
     body += ["s_sub_u32 s61, s61, 1", "s_cmp_lg_u32 s61, 0",
              "s_cbranch_scc1 L_loop_%="]
     body += epilogue()
@@ -186,18 +205,21 @@ def build(dt):
 
 def main():
     out = sys.argv[1]
-    dts = ["f16", "bf16"]
     with open(out, "w") as f:
         f.write("// generated by gen_k4w.py -- do not edit\n")
-        for dt in dts:
-            body = build(dt)
-            # bf16 epilogue converts with v_cvt_pk_bf16_f32
-            if dt == "bf16":
-                body = [b.replace("v_cvt_pk_f16_f32", "v_cvt_pk_bf16_f32") for b in body]
-            f.write(f"#define K4W_ASM_{dt.upper()} \\\n")
-            for ins in body:
-                f.write(f'  "{ins}\\n" \\\n')
-            f.write("  \"\"\n\n")
+        for v, opt in VARIANTS.items():
+            for dt in ("f16", "bf16"):
+                if dt == "bf16" and v != 0:
+                    continue
+                body = build(dt, opt)
+                if dt == "bf16":
+                    body = [b.replace("v_cvt_pk_f16_f32", "v_cvt_pk_bf16_f32")
+                            for b in body]
+                f.write(f"#define K4W_ASM_{dt.upper()}_V{v} \\\n")
+                for ins in body:
+                    f.write(f'  "{ins}\\n" \\\n')
+                f.write("  \"\"\n\n")
+        f.write(f"#define K4W_NVARIANTS {len(VARIANTS)}\n")
         clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(128, 256)]
                 + [f'"s{i}"' for i in range(40, 80)] + ['"scc"', '"memory"'])
         f.write("#define K4W_CLOBBERS " + ", ".join(clob) + "\n")

@@ -40,7 +40,7 @@ __device__ __forceinline__ int sload_short(const short *base, int e) {
   return ((a & 2) ? (v >> 16) : v) & 0xffff;
 }
 
-template <bool kBf16>
+template <bool kBf16, int kVar>
 __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
   __shared__ __attribute__((aligned(1024))) char lds[163840];
   const int tid = threadIdx.x;
@@ -120,9 +120,35 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
     [vrd4] "v"(vrd[4]), [vrd5] "v"(vrd[5]), [vrd6] "v"(vrd[6]),             \
     [vrd7] "v"(vrd[7]), [vw0] "v"(vw0), [vw1] "v"(vw1)
   if constexpr (kBf16)
-    asm volatile(K4W_ASM_BF16 : K4W_OPERANDS : K4W_CLOBBERS);
+    asm volatile(K4W_ASM_BF16_V0 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 0)
+    asm volatile(K4W_ASM_F16_V0 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 1)
+    asm volatile(K4W_ASM_F16_V1 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 2)
+    asm volatile(K4W_ASM_F16_V2 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 3)
+    asm volatile(K4W_ASM_F16_V3 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 4)
+    asm volatile(K4W_ASM_F16_V4 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 5)
+    asm volatile(K4W_ASM_F16_V5 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 6)
+    asm volatile(K4W_ASM_F16_V6 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 7)
+    asm volatile(K4W_ASM_F16_V7 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 8)
+    asm volatile(K4W_ASM_F16_V8 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 9)
+    asm volatile(K4W_ASM_F16_V9 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 10)
+    asm volatile(K4W_ASM_F16_V10 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 11)
+    asm volatile(K4W_ASM_F16_V11 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 12)
+    asm volatile(K4W_ASM_F16_V12 : K4W_OPERANDS : K4W_CLOBBERS);
   else
-    asm volatile(K4W_ASM_F16 : K4W_OPERANDS : K4W_CLOBBERS);
+    asm volatile(K4W_ASM_F16_V13 : K4W_OPERANDS : K4W_CLOBBERS);
   __syncthreads();
   // staging [128][1040 B] -> C, 16-byte nontemporal stores
   for (int id = tid; id < 128 * 64; id += 256) {
@@ -140,7 +166,7 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
 
 extern "C" int k4w_dsd(const void *s_data, const int *offsets, const short *indices,
                        const void *d, void *c, int m, int k, int n, int bf16,
-                       hipStream_t stream) {
+                       int variant, hipStream_t stream) {
   K4wParams p;
   p.s_data = (const char *)s_data;
   p.s_offsets = offsets;
@@ -154,9 +180,22 @@ extern "C" int k4w_dsd(const void *s_data, const int *offsets, const short *indi
   p.j_limit = n;
   const int grid = p.num_rows * p.num_jtiles;
   (void)k;
-  if (bf16)
-    hipLaunchKernelGGL(k4w_dsd_nn<true>, dim3(grid), dim3(256), 0, stream, p);
-  else
-    hipLaunchKernelGGL(k4w_dsd_nn<false>, dim3(grid), dim3(256), 0, stream, p);
+#define K4W_LAUNCH(B, V) \
+  hipLaunchKernelGGL((k4w_dsd_nn<B, V>), dim3(grid), dim3(256), 0, stream, p)
+  if (bf16) K4W_LAUNCH(true, 0);
+  else if (variant == 1) K4W_LAUNCH(false, 1);
+  else if (variant == 2) K4W_LAUNCH(false, 2);
+  else if (variant == 3) K4W_LAUNCH(false, 3);
+  else if (variant == 4) K4W_LAUNCH(false, 4);
+  else if (variant == 5) K4W_LAUNCH(false, 5);
+  else if (variant == 6) K4W_LAUNCH(false, 6);
+  else if (variant == 7) K4W_LAUNCH(false, 7);
+  else if (variant == 8) K4W_LAUNCH(false, 8);
+  else if (variant == 9) K4W_LAUNCH(false, 9);
+  else if (variant == 10) K4W_LAUNCH(false, 10);
+  else if (variant == 11) K4W_LAUNCH(false, 11);
+  else if (variant == 12) K4W_LAUNCH(false, 12);
+  else if (variant == 13) K4W_LAUNCH(false, 13);
+  else K4W_LAUNCH(false, 0);
   return (int)hipGetLastError();
 }

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--variants", default="0")
     a = ap.parse_args()
     if a.build_only:
         build()
@@ -64,12 +65,12 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     bf = 1 if a.dtype == "bf16" else 0
 
-    def mine():
+    def mine(v=0):
         return lib.k4w_dsd(ctypes.c_void_p(prob.a_vals.data_ptr()),
                            ctypes.c_void_p(offs_t.data_ptr()),
                            ctypes.c_void_p(idx_t.data_ptr()),
                            ctypes.c_void_p(prob.b_vals.data_ptr()),
-                           ctypes.c_void_p(c2.data_ptr()), d, d, d, bf,
+                           ctypes.c_void_p(c2.data_ptr()), d, d, d, bf, v,
                            ctypes.c_void_p(stream))
 
     ship()
@@ -107,16 +108,20 @@ def main():
         ship()
         mine()
     torch.cuda.synchronize()
-    ts, tm = [], []
+    variants = [int(v) for v in a.variants.split(",")] if a.variants else [0]
+    fns = {"shipped": ship}
+    for v in variants:
+        fns[f"k4w_v{v}"] = (lambda v=v: mine(v))
+    times = {k: [] for k in fns}
     for _ in range(a.rounds):
-        ts.append(timed(ship, a.calls))
-        tm.append(timed(mine, a.calls))
+        for k, fn in fns.items():
+            times[k].append(timed(fn, a.calls))
     flops = prob.flops
-    out = {"density": a.density, "uniform": a.uniform, "dtype": a.dtype,
-           "shipped_us": sorted(ts)[len(ts) // 2], "k4w_us": sorted(tm)[len(tm) // 2],
-           "shipped_all": [round(x, 2) for x in ts], "k4w_all": [round(x, 2) for x in tm]}
-    out["shipped_tflops"] = round(flops / out["shipped_us"] / 1e6, 1)
-    out["k4w_tflops"] = round(flops / out["k4w_us"] / 1e6, 1)
+    out = {"density": a.density, "uniform": a.uniform, "dtype": a.dtype}
+    for k, ts in times.items():
+        med = sorted(ts)[len(ts) // 2]
+        out[k] = {"us": round(med, 2), "tflops": round(flops / med / 1e6, 1),
+                  "min": round(min(ts), 2)}
     print(json.dumps(out), flush=True)
 
 

@@ -1,0 +1,73 @@
+"""Same-process A/B of the DSD NN kernels: the 4-wave hand-scheduled kernel
+(dsd4w.hip) vs the 8-wave block_gemm_kernel, on the headline problem
+(bench.py's DsdProblem, 4096^3, random uniform topology) at each density.
+Interleaved rounds of `calls` back-to-back launches; medians.
+
+python scripts/ab_dsd4w.py [--densities 0.5,0.1,0.3,0.9] [--rounds 7]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--densities", default="0.5,0.1,0.3,0.9")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--calls", type=int, default=50)
+    ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--dim", type=int, default=4096)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import bench
+    import sputnik_amd as sp
+    from sputnik_amd import matrix_utils as mu
+
+    dev = torch.device("cuda:0")
+    d = a.dim
+    for dens in [float(x) for x in a.densities.split(",")]:
+        rng = np.random.default_rng(1)
+        nz = mu.nonzeros_for_density(d, d, dens)
+        off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
+        prob = bench.DsdProblem(d, d, off, idx, d, False, False, a.dtype, 7, dev)
+        fn = prob.launcher()
+
+        def timed(four):
+            sp.select_dsd_kernel(four)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.calls):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(e) * 1e3 / a.calls
+
+        for four in (2, 0, 2, 0):
+            timed(four)
+            for _ in range(100):
+                fn()
+        torch.cuda.synchronize()
+        t4, t8 = [], []
+        for _ in range(a.rounds):
+            t4.append(timed(2))
+            t8.append(timed(0))
+        sp.select_dsd_kernel(1)
+        med = lambda v: sorted(v)[len(v) // 2]
+        out = {"density": dens, "dtype": a.dtype, "dim": d,
+               "us_4wave": round(med(t4), 2), "us_8wave": round(med(t8), 2),
+               "tflops_4wave": round(prob.flops / med(t4) / 1e6, 1),
+               "tflops_8wave": round(prob.flops / med(t8) / 1e6, 1),
+               "all_4wave": [round(x, 2) for x in t4],
+               "all_8wave": [round(x, 2) for x in t8],
+               "pair_errors": sp.pair_errors()}
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -116,6 +116,7 @@ _SIGNATURES = {
     "sputnik_pair_errors": [],
     "sputnik_debug_pair_fault": [ctypes.c_int],
     "sputnik_capture_workspaces": [],
+    "sputnik_select_dsd_kernel": [ctypes.c_int],
 }
 _RESTYPES = {
     "sputnik_abi_block_matrix_size": ctypes.c_size_t,
@@ -413,6 +414,13 @@ def can_implement(op: str, a, transpose_a, b, transpose_b, c) -> bool:
         int(bool(transpose_b)), ctypes.byref(cc)))
 
 
+def select_dsd_kernel(four_wave: int = -1) -> int:
+    """DSD NN kernel choice (sputnik_select_dsd_kernel): 1 the 4-wave
+    hand-scheduled kernel where it pays (default), 2 wherever it applies, 0
+    the 8-wave kernel, -1 query only. Returns the previous choice."""
+    return int(lib().sputnik_select_dsd_kernel(int(four_wave)))
+
+
 def version() -> str:
     return lib().sputnik_version().decode()
 
@@ -427,6 +435,7 @@ __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
     "build_hash", "capture_workspaces", "pair_errors", "sdd_plan",
+    "select_dsd_kernel",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",

@@ -58,6 +58,11 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
 int PairErrors();
 void SetPairFault(int on);
 int CaptureWorkspaces();
+// DSD NN: 4-wave kernel on (1) / off (0) / forced regardless of density
+// (2); -1 queries. Returns the previous.
+int SelectDsdKernel(int four_wave);
+bool Dsd4wEnabled();
+bool Dsd4wForced();
 
 }  // namespace sputnik_amd
 

@@ -271,6 +271,10 @@ int sputnik_capture_workspaces(void) {
   return sputnik_amd::CaptureWorkspaces();
 }
 
+int sputnik_select_dsd_kernel(int four_wave) {
+  return sputnik_amd::SelectDsdKernel(four_wave);
+}
+
 size_t sputnik_abi_block_matrix_size(void) { return sizeof(BlockMatrix); }
 
 size_t sputnik_abi_block_matrix_offset(int field) {

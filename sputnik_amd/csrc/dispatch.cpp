@@ -24,6 +24,7 @@
 
 #include "api_internal.h"
 #include "block_gemm.h"
+#include "dsd4w.h"
 #include "metadata.h"
 #include "sputnik/sputnik.h"
 #include "sputnik_amd.h"
@@ -373,6 +374,30 @@ int PairErrors() {
 }
 
 void SetPairFault(int on) { g_pair_fault = on != 0; }
+
+// DSD NN kernel selection: the 4-wave hand-scheduled kernel (dsd4w.hip) where
+// it applies, else the 8-wave block_gemm_kernel. SPUTNIK_AMD_DSD4W=0 (or
+// sputnik_select_dsd_kernel(0), tests and A/B) keeps the 8-wave kernel.
+static std::atomic<int> g_dsd4w{-1};
+static int Dsd4wMode() {
+  int v = g_dsd4w.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
+    v = e != nullptr ? std::atoi(e) : 1;
+    v = v < 0 ? 1 : (v > 2 ? 2 : v);
+    g_dsd4w.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
+bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
+// 2: wherever the kernel can run, whatever the density (tests).
+bool Dsd4wForced() { return Dsd4wMode() == 2; }
+int SelectDsdKernel(int four_wave) {
+  const int prev = Dsd4wMode();
+  if (four_wave >= 0)
+    g_dsd4w.store(four_wave > 2 ? 2 : four_wave, std::memory_order_relaxed);
+  return prev;
+}
 
 static void ReclaimCaptureSlots() {
   for (auto &sl : g_capture_pairs) {
@@ -851,6 +876,10 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   p.debug = g_debug;
   PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
   const bool tall = UseTall(&p, stream);
+  if (Dsd4wEnabled() &&
+      Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
+                   !ta, tb, false, tall))
+    return LaunchDsd4w(dtype, p, stream);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 
@@ -1198,7 +1227,10 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 }  // namespace sputnik_amd
 
 // Experiment hook (not part of include/sputnik_amd.h): per-segment cycle
-// sums / timelines of SPUTNIK_EXP & 128 / 512 builds.
+// sums / timelines of SPUTNIK_EXP & 128 / 512 builds (scripts/exp_build.sh).
+// Only experiment builds export it; the shipped library has no such entry.
+#if SPUTNIK_EXP != 0
 extern "C" void sputnik_exp_set_debug(void *buffer) {
   sputnik_amd::g_debug = static_cast<unsigned long long *>(buffer);
 }
+#endif

@@ -1,0 +1,28 @@
+// sputnik-amd: the 4-wave hand-scheduled DSD NN kernel (dsd4w.hip).
+#ifndef SPUTNIK_AMD_DSD4W_H_
+#define SPUTNIK_AMD_DSD4W_H_
+
+#include <hip/hip_runtime.h>
+
+#include "block_gemm.h"
+
+namespace sputnik_amd {
+
+// Whether the 4-wave kernel serves this prepared launch: DSD with S
+// k-contiguous (A not transposed) and D n-contiguous (B not transposed),
+// straight output, on the one-tile-per-CU 128 x 512 launch (plain or pair
+// balanced; not split mode, not persistent, not the tall configuration).
+// blocks: stored blocks of the sparse operand; below a mean of
+// kDsd4wMinMean blocks per block-row the 8-wave kernel is faster (its fixed
+// per-tile costs are shared by twice the waves; r04 A/B).
+constexpr int kDsd4wMinMean = 12;
+bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
+                  bool out_t, bool tall);
+
+// Launches it; p as prepared for the 8-wave kernel (PrepareDsd +
+// PreparePairs): the same grid, workspaces and epochs.
+hipError_t LaunchDsd4w(int dtype, const GemmParams &p, hipStream_t stream);
+
+}  // namespace sputnik_amd
+
+#endif  // SPUTNIK_AMD_DSD4W_H_

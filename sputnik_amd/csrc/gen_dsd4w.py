@@ -1,0 +1,348 @@
+"""Generates dsd4w_asm.inc: the hand-scheduled body of the 4-wave DSD kernel
+(dsd4w.hip). Run by the Makefile; the output is committed too, and
+tests/test_abi.py checks that it matches this generator.
+
+Why a generator: the k-loop interleaves, per 32-deep k-step and wave, 64
+v_mfma_f32_16x16x32_{f16,bf16} with 24 LDS fragment reads and 10 LDS-DMA
+instructions on fixed registers. hipcc cannot be made to keep that schedule
+(at 8 waves x 256 VGPRs every change of the step structure spilled, DESIGN
+§3.1), so the whole body -- prologue, k-loop, pair publish, pair collect and
+the accumulator -> fp16/bf16 staging -- is ONE inline-asm statement with
+literal registers, and the HIP code around it only computes operands and
+copies the staged tile out.
+
+Tile: one workgroup = 4 waves (one per SIMD) owns a 128 x 512 output tile of
+DSD C = A . B (A's 128-row block-row times a 512-column panel of B); wave w
+owns columns [128 w, 128 w + 128) as 8 x 8 accumulators of 16 x 16 (fp32, in
+a[0:255]). The MFMA computes the tile transposed (B fragment as the A
+operand), so a lane's 4 accumulator values are 4 consecutive columns of one
+output row -- the layout of the 8-wave kernel (block_gemm.h mfma_step), so the
+two kernels' products are bit-identical on unpaired rows.
+
+Per k-step (32 deep), each wave:
+  * 64 MFMAs on fragment set (step % 2);
+  * in their gaps: 16 ds_read_b64_tr_b16 (its 8 D fragments of step + 1,
+    from its private D image) and 8 ds_read_b128 (the 8 S fragments, from
+    the S image all four waves share) into the other set;
+  * 10 LDS-DMA (buffer_load_dwordx4 ... lds) of step + 3: 8 KiB of its own D
+    image and 2 KiB of the shared S image;
+  * one s_barrier (the S image of step + 1 is written by all waves).
+LDS (160 KiB): S ring 4 x 8 KiB at [0, 32K); wave w's D ring 4 x 8 KiB at
+32K + 32K w. Images and swizzles are block_gemm.h's (kc_key / tr_key):
+S [128 rows][32 k] with 16-byte chunk c ^ ((row >> 1) & 3), D [32 k][128 cols]
+with 32-byte sector s ^ tr_key(k), both applied on the DMA source address.
+
+Register map (literal, declared as clobbers):
+  a[0:255]                accumulators, acc(m, n) = a[4 (8 m + n) : +3]
+  v[128:159] / v[160:191] S / D fragments, set 0
+  v[192:223] / v[224:255] S / D fragments, set 1
+  v[96:127]               epilogue / poll temporaries
+  s[40:43] S-block buffer descriptor, s[44:47] D descriptor,
+  s[84:87] pair-partial descriptor, s56..s79, s94..s99 loop state.
+Everything read-only comes in as an operand (%[name]).
+
+Sparse-row segments (pair balancing, dispatch.cpp PreparePairs): a virtual
+entry x in [0, ntot) is the CSR entry x + (x < n1 ? b1 : b2m) (b2m = b2 - n1).
+A pair producer runs the heavy row's head [0, n1) and publishes its fp32
+partial when `remaining blocks == flushrem` (= n2), then its own row; a
+consumer (collect != 0) adds the published partial in the epilogue.
+
+Usage: python gen_dsd4w.py OUT.inc
+"""
+import sys
+
+FS = (128, 192)
+FD = (160, 224)
+SLOT = 8192
+DMA_POS = [3, 9, 15, 21, 27, 33, 39, 45, 51, 57]
+D_READS_AT = 2
+BARRIER_AT = 18
+S_READS_AT = 19
+NAN_F16 = "0x7e007e00"
+NAN_BF16 = "0x7fc07fc0"
+WAIT_TICKS = 20000000   # s_memrealtime (100 MHz): 0.2 s (block_gemm.h kPairWaitTicks)
+
+
+def mfma(dt, m, n, s, zero_c=False):
+    a = 4 * (8 * m + n)
+    c = "0" if zero_c else f"a[{a}:{a + 3}]"
+    return (f"v_mfma_f32_16x16x32_{dt} a[{a}:{a + 3}], "
+            f"v[{FD[s] + 4 * n}:{FD[s] + 4 * n + 3}], "
+            f"v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], {c}")
+
+
+def d_reads(slot, s):
+    out = []
+    for n in range(8):
+        b = FD[s] + 4 * n
+        out.append(f"ds_read_b64_tr_b16 v[{b}:{b + 1}], %[vrd{n}] offset:{slot * SLOT}")
+        out.append(f"ds_read_b64_tr_b16 v[{b + 2}:{b + 3}], %[vrd{n}] "
+                   f"offset:{slot * SLOT + 1024}")
+    return out
+
+
+def s_reads(slot, s):
+    return [f"ds_read_b128 v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], %[vrs] "
+            f"offset:{slot * SLOT + m * 1024}" for m in range(8)]
+
+
+def dmas(slot):
+    """(m0 setup, load) pairs of one step's 10 LDS-DMAs into ring slot `slot`:
+    2 x 1 KiB of the shared S image (16 rows each), 8 x 1 KiB of the wave's D
+    image (4 k-rows each)."""
+    out = []
+    for q in range(2):
+        out.append((f"s_add_u32 m0, %[ms], {slot * SLOT + q * 1024}",
+                    f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} "
+                    f"offen lds"))
+    for q in range(8):
+        out.append((f"s_add_u32 m0, %[md], {slot * SLOT + q * 1024}",
+                    f"buffer_load_dwordx4 %[vd{(q >> 1) & 1}], s[44:47], s{64 + q} "
+                    f"offen lds"))
+    return out
+
+
+# The fed block advances one k-step: S by 64 B (32 k of a 256-B row), D by
+# 32 rows.
+ADVANCE = ["s_add_u32 s40, s40, 64", "s_addc_u32 s41, s41, 0",
+           "s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
+
+
+def entry_of(xreg, out_reg):
+    """out_reg = absolute CSR entry of virtual entry xreg (scc clobbered)."""
+    return [f"s_cmp_lt_u32 {xreg}, %[n1]",
+            f"s_cselect_b32 {out_reg}, %[b1], %[b2m]",
+            f"s_add_u32 {out_reg}, {out_reg}, {xreg}"]
+
+
+# Switch the fed block to the next virtual entry (s57 + 1, clamped to the
+# last): S block = its entry (storage order), D rows = 128 x its k-block
+# (s58, loaded a block ahead); then s58 <- the k-block the index prefetch
+# brought in (s59 >> s60).
+SWITCH = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
+          + entry_of("s57", "s76")
+          + ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15",
+             "s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
+             "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
+             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
+             "s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"])
+
+# Scalar load of the k-block (int16) of virtual entry min(s56, xlast) into
+# s59 (its half in s60), one block ahead of the SWITCH that uses it.
+IDX_LOAD = (["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"]
+            + entry_of("s78", "s79")
+            + ["s_lshl_b32 s79, s79, 1", "s_and_b32 s60, s79, 2",
+               "s_lshl_b32 s60, s60, 3", "s_and_b32 s79, s79, 0xfffffffc",
+               "s_add_u32 s76, %[ixlo], s79", "s_addc_u32 s77, %[ixhi], 0",
+               "s_load_dword s59, s[76:77], 0x0"])
+
+
+def step(dt, H, zero_c=False):
+    """Step H of a block: MFMAs on set H % 2; reads of step + 1 from slot
+    (H + 1) % 4 into the other set; DMA of step + 3 into slot (H + 3) % 4
+    (H = 0: the fed block's last step; H = 1..3: steps 0..2 of the next
+    block, switched to at H = 1)."""
+    cur, nxt = H % 2, 1 - H % 2
+    gaps = [[] for _ in range(64)]
+    if H == 0:
+        gaps[0] += IDX_LOAD
+    # own DMA of step + 1 landed (step + 2's 10 may still fly)
+    gaps[1].append("s_waitcnt vmcnt(10)")
+    if H == 1:
+        gaps[1] += SWITCH
+    for i, ins in enumerate(d_reads((H + 1) % 4, nxt)):
+        gaps[D_READS_AT + i].append(ins)
+    # every wave's S DMA of step + 1 landed (each waited above) / every wave
+    # done reading the slot refilled below (its reads were waited at the end
+    # of step - 2)
+    gaps[BARRIER_AT].append("s_barrier")
+    for i, ins in enumerate(s_reads((H + 1) % 4, nxt)):
+        gaps[S_READS_AT + i].append(ins)
+    for (m0, ld), k in zip(dmas((H + 3) % 4), DMA_POS):
+        gaps[k - 1].append(m0)
+        gaps[k].append(ld)
+    if H != 0:
+        gaps[58] += ADVANCE
+    gaps[63].append("s_waitcnt lgkmcnt(0)")
+    out = []
+    for i in range(64):
+        out.append(mfma(dt, i // 8, i % 8, cur, zero_c))
+        out += gaps[i]
+    return out
+
+
+def prologue():
+    out = ["s_mov_b32 s42, 0x7fffffff", "s_mov_b32 s43, 0x00020000",
+           "s_mov_b32 s46, 0x7fffffff", "s_mov_b32 s47, 0x00020000",
+           "s_mov_b32 s84, %[pdlo]", "s_mov_b32 s85, %[pdhi]",
+           "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
+           "s_mov_b32 s56, 2", "s_mov_b32 s57, 0",
+           "s_mov_b32 s58, %[kb1]", "s_mov_b32 s61, %[ntot]",
+           "s_mov_b32 s72, 4096", "s_mov_b32 s64, 0"]
+    out += [f"s_mul_i32 s{64 + q}, %[k4], {q}" for q in range(1, 8)]
+    # block 0: virtual entry 0, k-block kb0
+    out += entry_of("s57", "s76")
+    out += ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15",
+            "s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
+            "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
+            "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
+    for slot in range(3):
+        for m0, ld in dmas(slot):
+            out += [m0, "s_nop 0", ld]
+        out += ADVANCE
+    out += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
+    out += ["s_waitcnt vmcnt(20)", "s_barrier"]
+    out += d_reads(0, 0) + s_reads(0, 0)
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def publish():
+    """Pair producer: the head partial (fp32, write-through sc1) to its slot,
+    every wave drained, one barrier, then the last wave's lane 0 raises the
+    flag (sc1) with this launch's epoch (the 8-wave kernel's protocol,
+    block_gemm.h publish / MI355X_MICROARCH hand-off table row 1)."""
+    out = ["s_nop 7", "s_nop 7", "s_nop 7"]
+    for i in range(64):
+        if i % 4 == 0:
+            out.append(f"s_mov_b32 s78, {(i // 4) * 4096}")
+        out.append(f"buffer_store_dwordx4 a[{4 * i}:{4 * i + 3}], %[vpl], s[84:87], s78 "
+                   f"offen offset:{(i % 4) * 1024} sc1")
+    out += ["s_waitcnt vmcnt(0)", "s_barrier",
+            "s_cmp_eq_u32 %[wave], 3", "s_cbranch_scc0 L_noflag_%=",
+            "s_cmp_lg_u32 %[pfault], 0", "s_cbranch_scc1 L_noflag_%=",
+            "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+            "v_mov_b32 v96, 0", "v_mov_b32 v97, %[epoch]",
+            "global_store_dword v96, v97, %[flag] sc1",
+            "s_mov_b64 exec, s[78:79]",
+            "L_noflag_%=:"]
+    return out
+
+
+def epilogue_body(cvt, mode):
+    """Accumulators -> staging image [128 rows][1040 B] (row 16 m + l % 16,
+    columns 128 w + 16 n + 4 (l / 16) .. + 3 at %[vw0] / %[vw1] + offset).
+    mode "plain"; "collect": + the published partial, streamed through
+    v[128:255] (32 fragments in flight, sc1 loads); "nan": NaN tile."""
+    out = []
+
+    def stage(i, src):
+        m, n = i // 8, i % 8
+        base = "%[vw0]" if m < 4 else "%[vw1]"
+        off = 16 * (m % 4) * 1040 + 32 * n
+        return f"ds_write_b64 {base}, {src} offset:{off}"
+
+    def load(i):
+        v = 128 + 4 * (i % 32)
+        return [f"s_mov_b32 s78, {(i // 4) * 4096}",
+                f"buffer_load_dwordx4 v[{v}:{v + 3}], %[vpl], s[84:87], s78 offen "
+                f"offset:{(i % 4) * 1024} sc1"]
+
+    if mode == "nan":
+        nan = NAN_F16 if cvt.endswith("f16_f32") else NAN_BF16
+        out += [f"v_mov_b32 v96, {nan}", "v_mov_b32 v97, v96"]
+        out += [stage(i, "v[96:97]") for i in range(64)]
+        return out
+    if mode == "collect":
+        for i in range(32):
+            out += load(i)
+    for i in range(64):
+        t = 96 + 8 * (i % 4)
+        a = 4 * i
+        out += [f"v_accvgpr_read_b32 v{t + j}, a{a + j}" for j in range(4)]
+        if mode == "collect":
+            out.append(f"s_waitcnt vmcnt({min(31, 63 - i)})")
+            p = 128 + 4 * (i % 32)
+            out += [f"v_add_f32 v{t + j}, v{t + j}, v{p + j}" for j in range(4)]
+            if i + 32 < 64:
+                out += load(i + 32)
+        out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}"]
+        out.append(stage(i, f"v[{t + 4}:{t + 5}]"))
+    return out
+
+
+def poll():
+    """Consumer: wait (bounded, s_memrealtime) for the producer's flag =
+    this launch's epoch; every wave polls for itself (each adds only its own
+    part of the partial). On time-out wave 0 counts the error and the tile
+    becomes NaN."""
+    return ["s_memrealtime s[96:97]", "s_waitcnt lgkmcnt(0)",
+            "L_poll_%=:",
+            "v_mov_b32 v96, 0",
+            "global_load_dword v97, v96, %[flag] sc1",
+            "s_waitcnt vmcnt(0)", "s_nop 0",
+            "v_readfirstlane_b32 s98, v97",
+            "s_cmp_eq_u32 s98, %[epoch]", "s_cbranch_scc1 L_got_%=",
+            "s_sleep 1",
+            "s_memrealtime s[98:99]", "s_waitcnt lgkmcnt(0)",
+            "s_sub_u32 s98, s98, s96", "s_subb_u32 s99, s99, s97",
+            "s_cmp_lg_u32 s99, 0", "s_cbranch_scc1 L_timeout_%=",
+            f"s_cmp_lt_u32 s98, {WAIT_TICKS}", "s_cbranch_scc1 L_poll_%=",
+            "L_timeout_%=:",
+            "s_cmp_eq_u32 %[wave], 0", "s_cbranch_scc0 L_nan_%=",
+            "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+            "v_mov_b32 v96, 0", "v_mov_b32 v97, 1",
+            "global_atomic_add v96, v97, %[err]",
+            "s_waitcnt vmcnt(0)",
+            "s_mov_b64 exec, s[78:79]",
+            "s_branch L_nan_%="]
+
+
+def build(dt):
+    cvt = f"v_cvt_pk_{dt}_f32"
+    body = prologue()
+    body.append("L_loop_%=:")
+    body += step(dt, 0)
+    body.append("L_mid_%=:")
+    for H in (1, 2, 3):
+        body += step(dt, H)
+    body += ["s_sub_u32 s61, s61, 1",
+             "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%=",
+             "s_cmp_lg_u32 s61, 0", "s_cbranch_scc1 L_loop_%=",
+             "s_branch L_exit_%="]
+    body.append("L_pub_%=:")
+    body += publish()
+    body += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_zero_%="]
+    body += step(dt, 0, zero_c=True)
+    body.append("s_branch L_mid_%=")
+    body.append("L_zero_%=:")
+    body += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
+    body.append("L_exit_%=:")
+    # every DMA landed (the loop's last three steps fed clamped dummies) and
+    # every wave's reads are done: the LDS is free for the staging image
+    body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7",
+             "s_cmp_lg_u32 %[collect], 0", "s_cbranch_scc1 L_collect_%="]
+    body += epilogue_body(cvt, "plain")
+    body.append("s_branch L_done_%=")
+    body.append("L_collect_%=:")
+    body += poll()
+    body.append("L_got_%=:")
+    body += epilogue_body(cvt, "collect")
+    body.append("s_branch L_done_%=")
+    body.append("L_nan_%=:")
+    body += epilogue_body(cvt, "nan")
+    body += ["L_done_%=:", "s_waitcnt lgkmcnt(0)"]
+    return body
+
+
+def render():
+    lines = ["// generated by sputnik_amd/csrc/gen_dsd4w.py -- do not edit", ""]
+    for dt in ("f16", "bf16"):
+        lines.append(f"#define DSD4W_ASM_{dt.upper()} \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt)]
+        lines += ['  ""', ""]
+    clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
+            + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]
+            + [f'"s{i}"' for i in range(84, 88)] + [f'"s{i}"' for i in range(96, 100)]
+            + ['"scc"', '"vcc"', '"memory"'])
+    lines.append("#define DSD4W_CLOBBERS " + ", ".join(clob))
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    with open(sys.argv[1], "w") as f:
+        f.write(render())
+
+
+if __name__ == "__main__":
+    main()

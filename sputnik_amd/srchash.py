@@ -17,7 +17,7 @@ def source_files(root=ROOT):
     out = []
     csrc = os.path.join(root, "sputnik_amd", "csrc")
     for name in sorted(os.listdir(csrc)):
-        if name.endswith((".h", ".hip", ".cpp")):
+        if name.endswith((".h", ".hip", ".cpp", ".inc", ".py")):
             out.append(os.path.join("sputnik_amd", "csrc", name))
     out.append(os.path.join("sputnik_amd", "Makefile"))
     inc = os.path.join(root, "include")

@@ -1,0 +1,116 @@
+"""GPU: the 4-wave hand-scheduled DSD NN kernel (sputnik_amd/csrc/dsd4w.hip)
+against the 8-wave kernel (block_gemm.h) and the oracle.
+
+Both kernels accumulate every output element over the same k-steps in the
+same order with the same MFMA instruction and operand roles, split paired
+rows at the same block and add the head partial the same way, so their
+outputs must be bit-identical (torch.equal) on every shape -- pair-balanced
+or not, partial column tiles, empty rows, both dtypes. The oracle check
+(north-star tolerance) pins the 4-wave kernel independently.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from sputnik_amd import matrix_utils as mu
+from tests import helpers as H
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import sputnik_amd as sp  # noqa: E402
+
+
+def _problem(m, k, n, density, dtype, seed, empty_rows=()):
+    rng = np.random.default_rng(seed)
+    R, C = m // 128, k // 128
+    nz = mu.nonzeros_for_density(m, k, density) // (128 * 128)
+    off, idx = mu.random_topology(R, C, nz, rng, unordered=True)
+    if empty_rows:
+        keep = ~np.isin(np.repeat(np.arange(R), np.diff(off)), empty_rows)
+        rows = np.repeat(np.arange(R), np.diff(off))[keep]
+        idx = idx[keep]
+        off = np.zeros(R + 1, np.int32)
+        np.cumsum(np.bincount(rows, minlength=R), out=off[1:])
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    nb = int(off[-1])
+    a = (torch.rand(max(nb, 1) * 16384, generator=g, device="cuda") * 2 - 1).to(td)
+    b = (torch.rand(k * n, generator=g, device="cuda") * 2 - 1).to(td)
+    A = sp.BlockMatrix(m, k, 128, nb * 16384, a,
+                       torch.from_numpy(np.asarray(off, np.int32)).cuda(),
+                       torch.from_numpy(np.asarray(idx).astype(np.int16)).cuda())
+    return A, sp.Matrix(k, n, b), off, idx, a, b
+
+
+def _run(A, B, m, n, dtype, four):
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+    prev = sp.select_dsd_kernel(2 if four else 0)
+    try:
+        sp.MatmulEx(A, False, B, False, sp.Matrix(m, n, c))
+        torch.cuda.synchronize()
+    finally:
+        sp.select_dsd_kernel(prev)
+    return c.view(m, n)
+
+
+CASES = [
+    # m, k, n, density
+    (4096, 4096, 4096, 0.5),    # headline: pairs, two panels per XCD
+    (4096, 4096, 4096, 0.1),
+    (4096, 4096, 4096, 0.3),
+    (4096, 4096, 4096, 0.9),
+    (2048, 4096, 4096, 0.5),    # 16 rows
+    (4096, 2048, 1032, 0.5),    # partial column tile, 3 panels
+    (4096, 1024, 264, 0.5),     # one narrow panel
+    (8192, 2048, 2048, 0.3),    # 64 rows: workgroup ranking (rank_block)
+    (1024, 4096, 4096, 0.05),   # few blocks per row: plain launch (no pairs)
+]
+
+
+@pytest.mark.parametrize("m,k,n,density", CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype):
+    A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
+    c4 = _run(A, B, m, n, dtype, True)
+    c8 = _run(A, B, m, n, dtype, False)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+
+
+def test_dsd4w_empty_rows_and_oracle():
+    """Empty block-rows get zero tiles; sampled rows against the oracle."""
+    m, k, n = 4096, 2048, 1024
+    A, B, off, idx, a, b = _problem(m, k, n, 0.5, "f16", seed=3,
+                                    empty_rows=(0, 5, 31))
+    c4 = _run(A, B, m, n, "f16", True)
+    c8 = _run(A, B, m, n, "f16", False)
+    assert torch.equal(c4, c8)
+    for r in (0, 5, 31):
+        assert torch.count_nonzero(c4[r * 128:(r + 1) * 128]) == 0
+    av = a.float().cpu().numpy().reshape(-1, 128, 128)
+    bv = b.float().cpu().numpy().reshape(k, n)
+    for r in (1, 17, 30):
+        o0, o1 = int(off[r]), int(off[r + 1])
+        row = np.zeros((128, k), np.float32)
+        for e in range(o0, o1):
+            row[:, idx[e] * 128:(idx[e] + 1) * 128] = av[e]
+        ref = O.gemm(row, False, bv, False, threads=H.oracle_threads())
+        H.assert_close(c4[r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
+                       "f16", f"dsd4w row-block {r}")
+
+
+def test_dsd4w_selector_roundtrip():
+    prev = sp.select_dsd_kernel(-1)
+    assert prev in (0, 1, 2)
+    assert sp.select_dsd_kernel(0) == prev
+    assert sp.select_dsd_kernel(-1) == 0
+    assert sp.select_dsd_kernel(prev) == 0
+    assert sp.select_dsd_kernel(-1) == prev
