@@ -48,15 +48,22 @@ def s_reads(slot, s):
     return out
 
 
-def dmas(slot):
+def dmas(slot, opt=None):
     """(m0 setup, load) pairs of one step's 10 DMAs into ring slot `slot`."""
+    opt = opt or {}
+    sd = "s[80:83]" if opt.get("s_fixed") else "s[40:43]"
+    dd = "s[84:87]" if opt.get("d_fixed") else "s[44:47]"
     out = []
     for q in range(2):
+        if opt.get("s_linear"):
+            out.append((f"s_add_u32 m0, s62, {slot * SLOT + q * 1024}",
+                        f"buffer_load_dwordx4 %[vsl], {sd}, {'0' if q == 0 else 's73'} offen lds"))
+            continue
         out.append((f"s_add_u32 m0, s62, {slot * SLOT + q * 1024}",
-                    f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} offen lds"))
+                    f"buffer_load_dwordx4 %[vs], {sd}, {'0' if q == 0 else 's72'} offen lds"))
     for q in range(8):
         out.append((f"s_add_u32 m0, s63, {slot * SLOT + q * 1024}",
-                    f"buffer_load_dwordx4 %[vd{(q >> 1) & 1}], s[44:47], s{64 + q} offen lds"))
+                    f"buffer_load_dwordx4 %[vd{(q >> 1) & 1}], {dd}, s{64 + q} offen lds"))
     return out
 
 
@@ -97,6 +104,12 @@ VARIANTS = {
     11: {"no_d_dma": True},
     12: {"no_vmcnt": True},
     13: {"no_lgkm": True},
+    14: {"s_fixed": True},
+    15: {"dma_pos": [1, 2, 9, 15, 21, 27, 33, 39, 45, 51]},
+    16: {"dma_pos": [45, 51, 3, 9, 15, 21, 27, 33, 39, 57]},
+    17: {"s_fixed": True, "d_fixed": True},
+    18: {"s_linear": True},
+    19: {"s_linear": True, "s_fixed": True},
 }
 
 
@@ -122,7 +135,7 @@ def step(dt, H, opt):
         sr = s_reads((H + 1) % 4, nxt)
         for i, ins in enumerate(sr):
             gaps[opt.get("s_reads_at", 19) + i].append(ins)
-    for j, ((m0, ld), k) in enumerate(zip(dmas((H + 3) % 4), opt.get("dma_pos", DMA_POS))):
+    for j, ((m0, ld), k) in enumerate(zip(dmas((H + 3) % 4, opt), opt.get("dma_pos", DMA_POS))):
         gaps[k - 1].append(m0)
         skip = (opt.get("no_dma") or (opt.get("no_s_dma") and j < 2)
                 or (opt.get("no_d_dma") and j >= 2))
@@ -152,7 +165,7 @@ def prologue():
         "s_add_u32 s56, %[e0], 2", "s_mov_b32 s57, %[e0]",
         "s_mov_b32 s58, %[kb1]", "s_mov_b32 s61, %[nblk]",
         "s_mov_b32 s62, %[ms]", "s_mov_b32 s63, %[md]",
-        "s_mov_b32 s72, 4096", "s_mov_b32 s74, %[elast]",
+        "s_mov_b32 s72, 4096", "s_mov_b32 s74, %[elast]", "s_mov_b32 s73, 1024",
         "s_mov_b32 s64, 0",
     ]
     for q in range(1, 8):
@@ -161,7 +174,9 @@ def prologue():
     out += ["s_lshl_b32 s76, s57, 15", "s_lshr_b32 s77, s57, 17",
             "s_add_u32 s40, s48, s76", "s_addc_u32 s41, s49, s77",
             "s_mul_i32 s76, %[kb0], s52", "s_mul_hi_u32 s77, %[kb0], s52",
-            "s_add_u32 s44, s50, s76", "s_addc_u32 s45, s51, s77"]
+            "s_add_u32 s44, s50, s76", "s_addc_u32 s45, s51, s77",
+            "s_mov_b64 s[80:81], s[40:41]", "s_mov_b64 s[82:83], s[42:43]",
+            "s_mov_b64 s[84:85], s[44:45]", "s_mov_b64 s[86:87], s[46:47]"]
     for slot in range(3):
         for m0, ld in dmas(slot):
             out += [m0, "s_nop 0", ld]
@@ -194,11 +209,13 @@ def epilogue():
 
 def build(dt, opt):
     body = prologue()
+    body += ["s_memtime %[t0]", "s_memrealtime %[r0]", "s_waitcnt lgkmcnt(0)"]
     body.append("L_loop_%=:")
     for H in range(4):
         body += step(dt, H, opt)
     body += ["s_sub_u32 s61, s61, 1", "s_cmp_lg_u32 s61, 0",
              "s_cbranch_scc1 L_loop_%="]
+    body += ["s_memtime %[t1]", "s_memrealtime %[r1]", "s_waitcnt lgkmcnt(0)"]
     body += epilogue()
     return body
 
@@ -221,7 +238,7 @@ def main():
                 f.write("  \"\"\n\n")
         f.write(f"#define K4W_NVARIANTS {len(VARIANTS)}\n")
         clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(128, 256)]
-                + [f'"s{i}"' for i in range(40, 80)] + ['"scc"', '"memory"'])
+                + [f'"s{i}"' for i in range(40, 88)] + ['"scc"', '"memory"'])
         f.write("#define K4W_CLOBBERS " + ", ".join(clob) + "\n")
 
 

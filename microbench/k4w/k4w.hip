@@ -19,6 +19,7 @@ struct K4wParams {
   int num_rows;
   int num_jtiles;
   int j_limit;
+  unsigned long long *debug;
 };
 
 __device__ __forceinline__ int tr_key(int k) {
@@ -43,6 +44,7 @@ __device__ __forceinline__ int sload_short(const short *base, int e) {
 template <bool kBf16, int kVar>
 __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
   __shared__ __attribute__((aligned(1024))) char lds[163840];
+  const unsigned long long r_entry = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -74,6 +76,7 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
   const int kb0 = sload_short(p.s_indices, e0);
   const int kb1 = sload_short(p.s_indices, e0 + 1 <= elast ? e0 + 1 : elast);
 
+  const uint32_t vsl = (uint32_t)(lane * 16 + wave * 2048);
   // S DMA: rows 32 w + l/4 (+16 for q = 1), chunk (l%4) ^ key(row)
   const int srow = 32 * wave + (lane >> 2);
   const uint32_t vs = (uint32_t)(srow * 256 + (((lane & 3) ^ ((srow >> 1) & 3)) << 4));
@@ -108,7 +111,9 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
   const uint32_t ms = lbase + 2048u * wave;
   const uint32_t md = lbase + 32768u + 32768u * wave;
 
+  unsigned long long t0 = 0, t1 = 0, r0 = 0, r1 = 0;
 #define K4W_OPERANDS                                                         \
+  [t0] "=&s"(t0), [t1] "=&s"(t1), [r0] "=&s"(r0), [r1] "=&s"(r1)              \
   : [sdlo] "s"((uint32_t)sd), [sdhi] "s"((uint32_t)(sd >> 32)),             \
     [dtlo] "s"((uint32_t)dt), [dthi] "s"((uint32_t)(dt >> 32)),             \
     [k128] "s"(k128), [k32] "s"(k32), [k4] "s"(k4),                          \
@@ -118,7 +123,7 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
     [vd0] "v"(vd[0]), [vd1] "v"(vd[1]), [vrs] "v"(vrs), [vrd0] "v"(vrd[0]), \
     [vrd1] "v"(vrd[1]), [vrd2] "v"(vrd[2]), [vrd3] "v"(vrd[3]),             \
     [vrd4] "v"(vrd[4]), [vrd5] "v"(vrd[5]), [vrd6] "v"(vrd[6]),             \
-    [vrd7] "v"(vrd[7]), [vw0] "v"(vw0), [vw1] "v"(vw1)
+    [vrd7] "v"(vrd[7]), [vw0] "v"(vw0), [vw1] "v"(vw1), [vsl] "v"(vsl)
   if constexpr (kBf16)
     asm volatile(K4W_ASM_BF16_V0 : K4W_OPERANDS : K4W_CLOBBERS);
   else if constexpr (kVar == 0)
@@ -147,8 +152,21 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
     asm volatile(K4W_ASM_F16_V11 : K4W_OPERANDS : K4W_CLOBBERS);
   else if constexpr (kVar == 12)
     asm volatile(K4W_ASM_F16_V12 : K4W_OPERANDS : K4W_CLOBBERS);
-  else
+  else if constexpr (kVar == 13)
     asm volatile(K4W_ASM_F16_V13 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 14)
+    asm volatile(K4W_ASM_F16_V14 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 15)
+    asm volatile(K4W_ASM_F16_V15 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 16)
+    asm volatile(K4W_ASM_F16_V16 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 17)
+    asm volatile(K4W_ASM_F16_V17 : K4W_OPERANDS : K4W_CLOBBERS);
+  else if constexpr (kVar == 18)
+    asm volatile(K4W_ASM_F16_V18 : K4W_OPERANDS : K4W_CLOBBERS);
+  else
+    asm volatile(K4W_ASM_F16_V19 : K4W_OPERANDS : K4W_CLOBBERS);
+  const unsigned long long r_asm = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   // staging [128][1040 B] -> C, 16-byte nontemporal stores
   for (int id = tid; id < 128 * 64; id += 256) {
@@ -160,13 +178,20 @@ __global__ void __launch_bounds__(256, 1) k4w_dsd_nn(const K4wParams p) {
         v, reinterpret_cast<v4u *>(p.c_data + ((long long)row * 128 + r) * p.c_ld +
                                    (long long)jc * 2));
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long r_end = __builtin_amdgcn_s_memrealtime();
+  if (p.debug != nullptr && tid == 0) {
+    unsigned long long *d = p.debug + blockIdx.x * 8;
+    d[0] = t0; d[1] = t1; d[2] = r0; d[3] = r1;
+    d[4] = r_entry; d[5] = r_asm; d[6] = r_end; d[7] = 0;
+  }
 }
 
 }  // namespace
 
 extern "C" int k4w_dsd(const void *s_data, const int *offsets, const short *indices,
                        const void *d, void *c, int m, int k, int n, int bf16,
-                       int variant, hipStream_t stream) {
+                       int variant, hipStream_t stream, void *debug) {
   K4wParams p;
   p.s_data = (const char *)s_data;
   p.s_offsets = offsets;
@@ -178,6 +203,7 @@ extern "C" int k4w_dsd(const void *s_data, const int *offsets, const short *indi
   p.num_rows = m / 128;
   p.num_jtiles = (n + 511) / 512;
   p.j_limit = n;
+  p.debug = (unsigned long long *)debug;
   const int grid = p.num_rows * p.num_jtiles;
   (void)k;
 #define K4W_LAUNCH(B, V) \
@@ -196,6 +222,12 @@ extern "C" int k4w_dsd(const void *s_data, const int *offsets, const short *indi
   else if (variant == 11) K4W_LAUNCH(false, 11);
   else if (variant == 12) K4W_LAUNCH(false, 12);
   else if (variant == 13) K4W_LAUNCH(false, 13);
+  else if (variant == 14) K4W_LAUNCH(false, 14);
+  else if (variant == 15) K4W_LAUNCH(false, 15);
+  else if (variant == 16) K4W_LAUNCH(false, 16);
+  else if (variant == 17) K4W_LAUNCH(false, 17);
+  else if (variant == 18) K4W_LAUNCH(false, 18);
+  else if (variant == 19) K4W_LAUNCH(false, 19);
   else K4W_LAUNCH(false, 0);
   return (int)hipGetLastError();
 }

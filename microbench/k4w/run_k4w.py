@@ -62,6 +62,8 @@ def main():
     offs_t = torch.from_numpy(np.asarray(off, np.int32)).to(dev)
     idx_t = torch.from_numpy(np.asarray(idx).astype(np.int16)).to(dev)
     c2 = torch.empty_like(prob.c_vals)
+    grid = R * (d // 512)
+    dbg = torch.zeros(grid * 8, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     bf = 1 if a.dtype == "bf16" else 0
 
@@ -71,7 +73,7 @@ def main():
                            ctypes.c_void_p(idx_t.data_ptr()),
                            ctypes.c_void_p(prob.b_vals.data_ptr()),
                            ctypes.c_void_p(c2.data_ptr()), d, d, d, bf, v,
-                           ctypes.c_void_p(stream))
+                           ctypes.c_void_p(stream), ctypes.c_void_p(dbg.data_ptr()))
 
     ship()
     rc = mine()
@@ -113,15 +115,36 @@ def main():
     for v in variants:
         fns[f"k4w_v{v}"] = (lambda v=v: mine(v))
     times = {k: [] for k in fns}
+    stamps = {}
     for _ in range(a.rounds):
         for k, fn in fns.items():
             times[k].append(timed(fn, a.calls))
+            if k != "shipped":
+                t = dbg.view(grid, 8).cpu().numpy().astype(np.float64)
+                steps = 4 * np.diff(off)[0] if a.uniform else 64
+                cyc = (t[:, 1] - t[:, 0])
+                clk = cyc / np.maximum(t[:, 3] - t[:, 2], 1) * 0.1  # GHz
+                e0 = t[:, 4].min()
+                tl = {"span_us": (t[:, 6].max() - e0) / 100,
+                      "entry_skew_us": (t[:, 4].max() - e0) / 100,
+                      "prologue_us": np.median(t[:, 2] - t[:, 4]) / 100,
+                      "loop_us": np.median(t[:, 3] - t[:, 2]) / 100,
+                      "asm_epi_us": np.median(t[:, 5] - t[:, 3]) / 100,
+                      "stores_us": np.median(t[:, 6] - t[:, 5]) / 100,
+                      "last_loop_end_us": (t[:, 3].max() - e0) / 100,
+                      "first_loop_end_us": (t[:, 3].min() - e0) / 100}
+                stamps.setdefault(k, []).append((np.median(cyc) / steps, np.median(clk), tl))
     flops = prob.flops
     out = {"density": a.density, "uniform": a.uniform, "dtype": a.dtype}
     for k, ts in times.items():
         med = sorted(ts)[len(ts) // 2]
         out[k] = {"us": round(med, 2), "tflops": round(flops / med / 1e6, 1),
                   "min": round(min(ts), 2)}
+        if k in stamps:
+            st = sorted(stamps[k])
+            out[k]["cyc_per_step"] = round(st[len(st) // 2][0], 1)
+            out[k]["ghz"] = round(float(np.median([x[1] for x in st])), 3)
+            out[k]["timeline"] = {kk: round(float(v), 2) for kk, v in st[len(st) // 2][2].items()}
     print(json.dumps(out), flush=True)
 
 

@@ -48,24 +48,24 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(e) * 1e3 / a.calls
 
-        for four in (2, 0, 2, 0):
-            timed(four)
+        arms = {"8wave": 0, "4wave": 2, "4wave_waveepi": 3}
+        for mode in arms.values():
+            timed(mode)
             for _ in range(100):
                 fn()
         torch.cuda.synchronize()
-        t4, t8 = [], []
+        ts = {k: [] for k in arms}
         for _ in range(a.rounds):
-            t4.append(timed(2))
-            t8.append(timed(0))
+            for k, mode in arms.items():
+                ts[k].append(timed(mode))
         sp.select_dsd_kernel(1)
         med = lambda v: sorted(v)[len(v) // 2]
-        out = {"density": dens, "dtype": a.dtype, "dim": d,
-               "us_4wave": round(med(t4), 2), "us_8wave": round(med(t8), 2),
-               "tflops_4wave": round(prob.flops / med(t4) / 1e6, 1),
-               "tflops_8wave": round(prob.flops / med(t8) / 1e6, 1),
-               "all_4wave": [round(x, 2) for x in t4],
-               "all_8wave": [round(x, 2) for x in t8],
-               "pair_errors": sp.pair_errors()}
+        out = {"density": dens, "dtype": a.dtype, "dim": d}
+        for k, v in ts.items():
+            out[k] = {"us": round(med(v), 2),
+                      "tflops": round(prob.flops / med(v) / 1e6, 1),
+                      "min": round(min(v), 2)}
+        out["pair_errors"] = sp.pair_errors()
         print(json.dumps(out), flush=True)
 
 

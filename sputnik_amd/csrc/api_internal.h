@@ -63,6 +63,7 @@ int CaptureWorkspaces();
 int SelectDsdKernel(int four_wave);
 bool Dsd4wEnabled();
 bool Dsd4wForced();
+bool Dsd4wWaveEpi();
 
 }  // namespace sputnik_amd
 

@@ -384,18 +384,20 @@ static int Dsd4wMode() {
   if (v < 0) {
     const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
     v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 2 ? 2 : v);
+    v = v < 0 ? 1 : (v > 3 ? 3 : v);
     g_dsd4w.store(v, std::memory_order_relaxed);
   }
   return v;
 }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2: wherever the kernel can run, whatever the density (tests).
-bool Dsd4wForced() { return Dsd4wMode() == 2; }
+// 2: wherever the kernel can run, whatever the density (tests); 3: the same
+// with the per-wave epilogue (A/B).
+bool Dsd4wForced() { return Dsd4wMode() >= 2; }
+bool Dsd4wWaveEpi() { return Dsd4wMode() == 3; }
 int SelectDsdKernel(int four_wave) {
   const int prev = Dsd4wMode();
   if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 2 ? 2 : four_wave, std::memory_order_relaxed);
+    g_dsd4w.store(four_wave > 3 ? 3 : four_wave, std::memory_order_relaxed);
   return prev;
 }
 
@@ -879,7 +881,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall))
-    return LaunchDsd4w(dtype, p, stream);
+    return LaunchDsd4w(dtype, p, Dsd4wWaveEpi(), stream);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 

@@ -21,7 +21,10 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 
 // Launches it; p as prepared for the 8-wave kernel (PrepareDsd +
 // PreparePairs): the same grid, workspaces and epochs.
-hipError_t LaunchDsd4w(int dtype, const GemmParams &p, hipStream_t stream);
+// wave_epi: every wave stages and stores its own 128 x 128 block (no
+// workgroup barrier at the end) instead of one workgroup-wide staging image.
+hipError_t LaunchDsd4w(int dtype, const GemmParams &p, bool wave_epi,
+                       hipStream_t stream);
 
 }  // namespace sputnik_amd
 

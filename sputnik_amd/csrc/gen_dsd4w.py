@@ -190,7 +190,7 @@ def prologue():
         for m0, ld in dmas(slot):
             out += [m0, "s_nop 0", ld]
         out += ADVANCE
-    out += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
+    # (no accumulator zeroing: the first step's MFMAs take C = 0)
     out += ["s_waitcnt vmcnt(20)", "s_barrier"]
     out += d_reads(0, 0) + s_reads(0, 0)
     out.append("s_waitcnt lgkmcnt(0)")
@@ -219,15 +219,22 @@ def publish():
     return out
 
 
-def epilogue_body(cvt, mode):
-    """Accumulators -> staging image [128 rows][1040 B] (row 16 m + l % 16,
-    columns 128 w + 16 n + 4 (l / 16) .. + 3 at %[vw0] / %[vw1] + offset).
-    mode "plain"; "collect": + the published partial, streamed through
-    v[128:255] (32 fragments in flight, sc1 loads); "nan": NaN tile."""
+def epilogue_body(cvt, mode, wave_epi=False):
+    """Accumulators -> staging image. Workgroup staging (wave_epi False):
+    [128 rows][1040 B] of the whole tile (row 16 m + l % 16, columns
+    128 w + 16 n + 4 (l / 16) .. + 3 at %[vw0] / %[vw1] + offset), copied out
+    by the HIP code after a barrier. Per-wave staging (wave_epi): the wave's
+    own 128 x 128 block in its own D ring region, [128 rows][256 B] with
+    16-byte chunk c of row r at c ^ (r & 15) (%[vws<n>] + 4096 m), then the
+    wave stores it itself (copy_out). mode "plain"; "collect": + the
+    published partial, streamed through v[128:255] (32 fragments in flight,
+    sc1 loads); "nan": NaN tile."""
     out = []
 
     def stage(i, src):
         m, n = i // 8, i % 8
+        if wave_epi:
+            return f"ds_write_b64 %[vws{n}], {src} offset:{4096 * m}"
         base = "%[vw0]" if m < 4 else "%[vw1]"
         off = 16 * (m % 4) * 1040 + 32 * n
         return f"ds_write_b64 {base}, {src} offset:{off}"
@@ -261,6 +268,31 @@ def epilogue_body(cvt, mode):
     return out
 
 
+def copy_out():
+    """Per-wave epilogue: the wave's staged 128 x 128 block -> C with 16-byte
+    nontemporal buffer stores, 4 rows x 256 B per instruction (lane l: row
+    4 i + l / 16, chunk l % 16; out-of-range columns carry an offset past
+    num_records and are dropped). C descriptor in s[84:87] (the partial's is
+    no longer needed), row offset 4 i ldc in s78."""
+    out = ["s_waitcnt lgkmcnt(0)",
+           "s_mov_b32 s84, %[cdlo]", "s_mov_b32 s85, %[cdhi]",
+           "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
+           "s_mov_b32 s78, 0"]
+    for b in range(8):
+        base = 96 + 16 * (b % 2)
+        idx = [4 * b + j for j in range(4)]
+        for j, i in enumerate(idx):
+            out.append(f"ds_read_b128 v[{base + 4 * j}:{base + 4 * j + 3}], "
+                       f"%[vrb{i % 4}] offset:{4096 * (i // 4)}")
+        out.append("s_waitcnt lgkmcnt(0)")
+        for j, i in enumerate(idx):
+            out += [f"buffer_store_dwordx4 v[{base + 4 * j}:{base + 4 * j + 3}], %[vco], "
+                    f"s[84:87], s78 offen nt",
+                    "s_add_u32 s78, s78, %[c4]"]
+        out.append("s_nop 1")
+    return out
+
+
 def poll():
     """Consumer: wait (bounded, s_memrealtime) for the producer's flag =
     this launch's epoch; every wave polls for itself (each adds only its own
@@ -288,9 +320,11 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt):
+def build(dt, wave_epi=False):
     cvt = f"v_cvt_pk_{dt}_f32"
     body = prologue()
+    # the first block's step 0 is the zero-C copy below (L_first)
+    body.append("s_branch L_first_%=")
     body.append("L_loop_%=:")
     body += step(dt, 0)
     body.append("L_mid_%=:")
@@ -303,34 +337,46 @@ def build(dt):
     body.append("L_pub_%=:")
     body += publish()
     body += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_zero_%="]
+    # step 0 of a block with the accumulators restarting from zero (C = 0):
+    # the launch's first step, and the first step after a pair publish
+    body.append("L_first_%=:")
     body += step(dt, 0, zero_c=True)
     body.append("s_branch L_mid_%=")
     body.append("L_zero_%=:")
     body += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
     body.append("L_exit_%=:")
-    # every DMA landed (the loop's last three steps fed clamped dummies) and
-    # every wave's reads are done: the LDS is free for the staging image
-    body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7",
-             "s_cmp_lg_u32 %[collect], 0", "s_cbranch_scc1 L_collect_%="]
-    body += epilogue_body(cvt, "plain")
+    if wave_epi:
+        # the wave's own DMAs (the loop's last three steps fed clamped
+        # dummies) landed and its reads are done: its D ring region is free
+        # (no other wave writes it), no barrier
+        body += ["s_waitcnt vmcnt(0)", "s_nop 7", "s_nop 7"]
+    else:
+        # every DMA landed and every wave's reads are done: the LDS is free
+        # for the staging image
+        body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
+    body += ["s_cmp_lg_u32 %[collect], 0", "s_cbranch_scc1 L_collect_%="]
+    body += epilogue_body(cvt, "plain", wave_epi)
     body.append("s_branch L_done_%=")
     body.append("L_collect_%=:")
     body += poll()
     body.append("L_got_%=:")
-    body += epilogue_body(cvt, "collect")
+    body += epilogue_body(cvt, "collect", wave_epi)
     body.append("s_branch L_done_%=")
     body.append("L_nan_%=:")
-    body += epilogue_body(cvt, "nan")
-    body += ["L_done_%=:", "s_waitcnt lgkmcnt(0)"]
+    body += epilogue_body(cvt, "nan", wave_epi)
+    body += ["L_done_%=:"]
+    body += copy_out() if wave_epi else ["s_waitcnt lgkmcnt(0)"]
     return body
 
 
 def render():
     lines = ["// generated by sputnik_amd/csrc/gen_dsd4w.py -- do not edit", ""]
     for dt in ("f16", "bf16"):
-        lines.append(f"#define DSD4W_ASM_{dt.upper()} \\")
-        lines += [f'  "{ins}\\n" \\' for ins in build(dt)]
-        lines += ['  ""', ""]
+        for wave_epi in (False, True):
+            name = f"DSD4W_ASM_{dt.upper()}" + ("_W" if wave_epi else "")
+            lines.append(f"#define {name} \\")
+            lines += [f'  "{ins}\\n" \\' for ins in build(dt, wave_epi)]
+            lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]
             + [f'"s{i}"' for i in range(84, 88)] + [f'"s{i}"' for i in range(96, 100)]

@@ -47,10 +47,13 @@ def _problem(m, k, n, density, dtype, seed, empty_rows=()):
     return A, sp.Matrix(k, n, b), off, idx, a, b
 
 
-def _run(A, B, m, n, dtype, four):
+def _run(A, B, m, n, dtype, mode):
+    """mode: 0 the 8-wave kernel, 2 the 4-wave kernel (workgroup epilogue),
+    3 the 4-wave kernel with the per-wave epilogue; 2 and 3 regardless of
+    the density gate."""
     td = torch.float16 if dtype == "f16" else torch.bfloat16
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
-    prev = sp.select_dsd_kernel(2 if four else 0)
+    prev = sp.select_dsd_kernel(mode)
     try:
         sp.MatmulEx(A, False, B, False, sp.Matrix(m, n, c))
         torch.cuda.synchronize()
@@ -75,23 +78,25 @@ CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype):
+@pytest.mark.parametrize("mode", [2, 3])
+def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
-    c4 = _run(A, B, m, n, dtype, True)
-    c8 = _run(A, B, m, n, dtype, False)
+    c4 = _run(A, B, m, n, dtype, mode)
+    c8 = _run(A, B, m, n, dtype, 0)
     assert not torch.isnan(c4.float()).any()
     assert torch.equal(c4, c8), (
         f"max diff {float((c4.float() - c8.float()).abs().max())}")
     assert sp.pair_errors() == 0
 
 
-def test_dsd4w_empty_rows_and_oracle():
+@pytest.mark.parametrize("mode", [2, 3])
+def test_dsd4w_empty_rows_and_oracle(mode):
     """Empty block-rows get zero tiles; sampled rows against the oracle."""
     m, k, n = 4096, 2048, 1024
     A, B, off, idx, a, b = _problem(m, k, n, 0.5, "f16", seed=3,
                                     empty_rows=(0, 5, 31))
-    c4 = _run(A, B, m, n, "f16", True)
-    c8 = _run(A, B, m, n, "f16", False)
+    c4 = _run(A, B, m, n, "f16", mode)
+    c8 = _run(A, B, m, n, "f16", 0)
     assert torch.equal(c4, c8)
     for r in (0, 5, 31):
         assert torch.count_nonzero(c4[r * 128:(r + 1) * 128]) == 0
@@ -109,7 +114,7 @@ def test_dsd4w_empty_rows_and_oracle():
 
 def test_dsd4w_selector_roundtrip():
     prev = sp.select_dsd_kernel(-1)
-    assert prev in (0, 1, 2)
+    assert prev in (0, 1, 2, 3)
     assert sp.select_dsd_kernel(0) == prev
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0
