@@ -179,9 +179,10 @@ void sputnik_debug_pair_fault(int on);
 int sputnik_capture_workspaces(void);
 /* DSD NN kernel choice (tests and same-process A/B): 1 = the 4-wave
  * hand-scheduled kernel where it applies and pays (the default; environment
- * SPUTNIK_AMD_DSD4W=0 turns it off), 2 = wherever it applies, whatever the
- * density, 0 = the 8-wave kernel everywhere, -1 = query only. Returns the
- * previous choice. Process-wide. */
+ * SPUTNIK_AMD_DSD4W=0 turns it off), 2 / 3 / 4 = wherever it applies,
+ * whatever the density, with its workgroup / per-wave / per-wave +
+ * specialized-last-block epilogue, 0 = the 8-wave kernel everywhere, -1 =
+ * query only. Returns the previous choice. Process-wide. */
 int sputnik_select_dsd_kernel(int four_wave);
 
 #ifdef __cplusplus

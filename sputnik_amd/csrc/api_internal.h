@@ -59,11 +59,11 @@ int PairErrors();
 void SetPairFault(int on);
 int CaptureWorkspaces();
 // DSD NN: 4-wave kernel on (1) / off (0) / forced regardless of density
-// (2); -1 queries. Returns the previous.
+// with epilogue 0, 1, 2 (2, 3, 4); -1 queries. Returns the previous.
 int SelectDsdKernel(int four_wave);
 bool Dsd4wEnabled();
 bool Dsd4wForced();
-bool Dsd4wWaveEpi();
+int Dsd4wEpi();
 
 }  // namespace sputnik_amd
 

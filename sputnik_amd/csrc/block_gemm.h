@@ -194,6 +194,9 @@ struct GemmParams {
   const int *d_offsets;
   const short *d_indices;
   const int *d_block_offsets;  // nullptr: storage block = entry
+  // Stored blocks of the sparse operand S (DSD: A's nonzeros / 128^2); the
+  // 4-wave DSD kernel preloads an index list this short (dsd4w.hip).
+  int s_blocks;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

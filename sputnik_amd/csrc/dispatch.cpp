@@ -384,20 +384,23 @@ static int Dsd4wMode() {
   if (v < 0) {
     const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
     v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 3 ? 3 : v);
+    v = v < 0 ? 1 : (v > 4 ? 4 : v);
     g_dsd4w.store(v, std::memory_order_relaxed);
   }
   return v;
 }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2: wherever the kernel can run, whatever the density (tests); 3: the same
-// with the per-wave epilogue (A/B).
+// 2..4: wherever the kernel can run, whatever the density (tests, A/B), with
+// epilogue 0 / 1 / 2 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
 bool Dsd4wForced() { return Dsd4wMode() >= 2; }
-bool Dsd4wWaveEpi() { return Dsd4wMode() == 3; }
+int Dsd4wEpi() {
+  const int m = Dsd4wMode();
+  return m >= 2 ? m - 2 : kDsd4wDefaultEpi;
+}
 int SelectDsdKernel(int four_wave) {
   const int prev = Dsd4wMode();
   if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 3 ? 3 : four_wave, std::memory_order_relaxed);
+    g_dsd4w.store(four_wave > 4 ? 4 : four_wave, std::memory_order_relaxed);
   return prev;
 }
 
@@ -501,6 +504,7 @@ Status PrepareDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   p->s_indices = static_cast<const short *>(ta ? a.indices_t : a.indices);
   p->s_block_offsets =
       ta ? static_cast<const int *>(a.block_offsets) : nullptr;
+  p->s_blocks = (int)(a.nonzeros / (kBlock * kBlock));
   p->d_data = static_cast<const char *>(b.data);
   p->d_ld = (long long)s.ldb * 2;
   p->c_data = static_cast<char *>(c.data);
@@ -881,7 +885,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall))
-    return LaunchDsd4w(dtype, p, Dsd4wWaveEpi(), stream);
+    return LaunchDsd4w(dtype, p, Dsd4wEpi(), stream);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 

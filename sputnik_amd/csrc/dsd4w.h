@@ -21,10 +21,12 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 
 // Launches it; p as prepared for the 8-wave kernel (PrepareDsd +
 // PreparePairs): the same grid, workspaces and epochs.
-// wave_epi: every wave stages and stores its own 128 x 128 block (no
-// workgroup barrier at the end) instead of one workgroup-wide staging image.
-hipError_t LaunchDsd4w(int dtype, const GemmParams &p, bool wave_epi,
-                       hipStream_t stream);
+// epi: 0 one workgroup-wide staging image copied out after a barrier; 1
+// every wave stages and stores its own 128 x 128 block (no barrier); 2 the
+// same with the last block specialized (no dummy DMA / reads, conversion
+// inside the final step's MFMAs).
+hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
+constexpr int kDsd4wDefaultEpi = 0;
 
 }  // namespace sputnik_amd
 

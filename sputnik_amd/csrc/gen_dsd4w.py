@@ -39,7 +39,10 @@ Register map (literal, declared as clobbers):
   v[96:127]               epilogue / poll temporaries
   s[40:43] S-block buffer descriptor, s[44:47] D descriptor,
   s[84:87] pair-partial descriptor, s56..s79, s94..s99 loop state.
-Everything read-only comes in as an operand (%[name]).
+Everything read-only comes in as an operand (%[name]); %[flags] packs the
+workgroup's role bits: 0 collect (pair consumer), 1 specialized last block
+allowed, 2 test fault (producer skips its flag), 3 last wave (raises the
+flag), 4 wave 0 (counts a time-out).
 
 Sparse-row segments (pair balancing, dispatch.cpp PreparePairs): a virtual
 entry x in [0, ntot) is the CSR entry x + (x < n1 ? b1 : b2m) (b2m = b2 - n1).
@@ -137,37 +140,61 @@ IDX_LOAD = (["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"]
                "s_load_dword s59, s[76:77], 0x0"])
 
 
-def step(dt, H, zero_c=False):
+def step(dt, H, zero_c=False, last=0, cvt=None):
     """Step H of a block: MFMAs on set H % 2; reads of step + 1 from slot
     (H + 1) % 4 into the other set; DMA of step + 3 into slot (H + 3) % 4
     (H = 0: the fed block's last step; H = 1..3: steps 0..2 of the next
-    block, switched to at H = 1)."""
+    block, switched to at H = 1).
+    last = H (1..3): step H of the launch's last block (per-wave epilogue
+    only): no DMA (there is no next block); step 2 waits for step 3's DMA
+    with vmcnt(0) (nothing younger in flight); step 3 reads nothing, meets
+    no barrier, and converts + stages each accumulator two MFMAs after its
+    final update (the per-wave staging region is the wave's own D ring,
+    whose last reads and DMAs are done)."""
     cur, nxt = H % 2, 1 - H % 2
     gaps = [[] for _ in range(64)]
     if H == 0:
         gaps[0] += IDX_LOAD
-    # own DMA of step + 1 landed (step + 2's 10 may still fly)
-    gaps[1].append("s_waitcnt vmcnt(10)")
-    if H == 1:
+    if last != 3:
+        # own DMA of step + 1 landed (step + 2's 10 may still fly)
+        gaps[1].append("s_waitcnt vmcnt(0)" if last == 2 else "s_waitcnt vmcnt(10)")
+    if H == 1 and not last:
         gaps[1] += SWITCH
-    for i, ins in enumerate(d_reads((H + 1) % 4, nxt)):
-        gaps[D_READS_AT + i].append(ins)
-    # every wave's S DMA of step + 1 landed (each waited above) / every wave
-    # done reading the slot refilled below (its reads were waited at the end
-    # of step - 2)
-    gaps[BARRIER_AT].append("s_barrier")
-    for i, ins in enumerate(s_reads((H + 1) % 4, nxt)):
-        gaps[S_READS_AT + i].append(ins)
-    for (m0, ld), k in zip(dmas((H + 3) % 4), DMA_POS):
-        gaps[k - 1].append(m0)
-        gaps[k].append(ld)
-    if H != 0:
-        gaps[58] += ADVANCE
-    gaps[63].append("s_waitcnt lgkmcnt(0)")
+    if last != 3:
+        for i, ins in enumerate(d_reads((H + 1) % 4, nxt)):
+            gaps[D_READS_AT + i].append(ins)
+        # every wave's S DMA of step + 1 landed (each waited above) / every
+        # wave done reading the slot refilled below (its reads were waited at
+        # the end of step - 2)
+        gaps[BARRIER_AT].append("s_barrier")
+        for i, ins in enumerate(s_reads((H + 1) % 4, nxt)):
+            gaps[S_READS_AT + i].append(ins)
+    if not last:
+        for (m0, ld), k in zip(dmas((H + 3) % 4), DMA_POS):
+            gaps[k - 1].append(m0)
+            gaps[k].append(ld)
+        if H != 0:
+            gaps[58] += ADVANCE
+    if last == 3:
+        for i in range(2, 64):
+            gaps[i] += convert(cvt, i - 2)
+    else:
+        gaps[63].append("s_waitcnt lgkmcnt(0)")
     out = []
     for i in range(64):
         out.append(mfma(dt, i // 8, i % 8, cur, zero_c))
         out += gaps[i]
+    return out
+
+
+def convert(cvt, i):
+    """Accumulator i (m = i / 8, n = i % 8) -> fp16 / bf16 pairs -> the
+    wave's staging region (per-wave layout, see epilogue_body)."""
+    t = 96 + 8 * (i % 4)
+    m, n = i // 8, i % 8
+    out = [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
+    out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}",
+            f"ds_write_b64 %[vws{n}], v[{t + 4}:{t + 5}] offset:{4096 * m}"]
     return out
 
 
@@ -209,8 +236,8 @@ def publish():
         out.append(f"buffer_store_dwordx4 a[{4 * i}:{4 * i + 3}], %[vpl], s[84:87], s78 "
                    f"offen offset:{(i % 4) * 1024} sc1")
     out += ["s_waitcnt vmcnt(0)", "s_barrier",
-            "s_cmp_eq_u32 %[wave], 3", "s_cbranch_scc0 L_noflag_%=",
-            "s_cmp_lg_u32 %[pfault], 0", "s_cbranch_scc1 L_noflag_%=",
+            "s_bitcmp1_b32 %[flags], 3", "s_cbranch_scc0 L_noflag_%=",
+            "s_bitcmp1_b32 %[flags], 2", "s_cbranch_scc1 L_noflag_%=",
             "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
             "v_mov_b32 v96, 0", "v_mov_b32 v97, %[epoch]",
             "global_store_dword v96, v97, %[flag] sc1",
@@ -311,7 +338,7 @@ def poll():
             "s_cmp_lg_u32 s99, 0", "s_cbranch_scc1 L_timeout_%=",
             f"s_cmp_lt_u32 s98, {WAIT_TICKS}", "s_cbranch_scc1 L_poll_%=",
             "L_timeout_%=:",
-            "s_cmp_eq_u32 %[wave], 0", "s_cbranch_scc0 L_nan_%=",
+            "s_bitcmp1_b32 %[flags], 4", "s_cbranch_scc0 L_nan_%=",
             "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
             "v_mov_b32 v96, 0", "v_mov_b32 v97, 1",
             "global_atomic_add v96, v97, %[err]",
@@ -320,7 +347,7 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt, wave_epi=False):
+def build(dt, wave_epi=False, last_block=False):
     cvt = f"v_cvt_pk_{dt}_f32"
     body = prologue()
     # the first block's step 0 is the zero-C copy below (L_first)
@@ -331,9 +358,22 @@ def build(dt, wave_epi=False):
     for H in (1, 2, 3):
         body += step(dt, H)
     body += ["s_sub_u32 s61, s61, 1",
-             "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%=",
-             "s_cmp_lg_u32 s61, 0", "s_cbranch_scc1 L_loop_%=",
+             "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%="]
+    if last_block:
+        # one block left and no publish or collect after it: the
+        # specialized last block (L_last)
+        body += ["s_cmp_eq_u32 s61, 1", "s_cbranch_scc0 L_cont_%=",
+                 "s_bitcmp1_b32 %[flags], 1", "s_cbranch_scc1 L_last_%=",
+                 "L_cont_%=:"]
+    body += ["s_cmp_lg_u32 s61, 0", "s_cbranch_scc1 L_loop_%=",
              "s_branch L_exit_%="]
+    if last_block:
+        body.append("L_last_%=:")
+        body += step(dt, 0)
+        for H in (1, 2, 3):
+            body += step(dt, H, last=H, cvt=cvt)
+        body += ["s_nop 7", "s_nop 7"] + convert(cvt, 62) + convert(cvt, 63)
+        body.append("s_branch L_done_%=")
     body.append("L_pub_%=:")
     body += publish()
     body += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_zero_%="]
@@ -354,7 +394,7 @@ def build(dt, wave_epi=False):
         # every DMA landed and every wave's reads are done: the LDS is free
         # for the staging image
         body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
-    body += ["s_cmp_lg_u32 %[collect], 0", "s_cbranch_scc1 L_collect_%="]
+    body += ["s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc1 L_collect_%="]
     body += epilogue_body(cvt, "plain", wave_epi)
     body.append("s_branch L_done_%=")
     body.append("L_collect_%=:")
@@ -372,10 +412,11 @@ def build(dt, wave_epi=False):
 def render():
     lines = ["// generated by sputnik_amd/csrc/gen_dsd4w.py -- do not edit", ""]
     for dt in ("f16", "bf16"):
-        for wave_epi in (False, True):
-            name = f"DSD4W_ASM_{dt.upper()}" + ("_W" if wave_epi else "")
+        for suffix, wave_epi, last_block in (("", False, False), ("_W", True, False),
+                                             ("_WL", True, True)):
+            name = f"DSD4W_ASM_{dt.upper()}{suffix}"
             lines.append(f"#define {name} \\")
-            lines += [f'  "{ins}\\n" \\' for ins in build(dt, wave_epi)]
+            lines += [f'  "{ins}\\n" \\' for ins in build(dt, wave_epi, last_block)]
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

@@ -49,8 +49,8 @@ def _problem(m, k, n, density, dtype, seed, empty_rows=()):
 
 def _run(A, B, m, n, dtype, mode):
     """mode: 0 the 8-wave kernel, 2 the 4-wave kernel (workgroup epilogue),
-    3 the 4-wave kernel with the per-wave epilogue; 2 and 3 regardless of
-    the density gate."""
+    3 with the per-wave epilogue, 4 per-wave + specialized last block; 2-4
+    regardless of the density gate."""
     td = torch.float16 if dtype == "f16" else torch.bfloat16
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
     prev = sp.select_dsd_kernel(mode)
@@ -78,7 +78,7 @@ CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("mode", [2, 3, 4])
 def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
     c4 = _run(A, B, m, n, dtype, mode)
@@ -89,7 +89,7 @@ def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     assert sp.pair_errors() == 0
 
 
-@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("mode", [2, 3, 4])
 def test_dsd4w_empty_rows_and_oracle(mode):
     """Empty block-rows get zero tiles; sampled rows against the oracle."""
     m, k, n = 4096, 2048, 1024
@@ -114,7 +114,7 @@ def test_dsd4w_empty_rows_and_oracle(mode):
 
 def test_dsd4w_selector_roundtrip():
     prev = sp.select_dsd_kernel(-1)
-    assert prev in (0, 1, 2, 3)
+    assert prev in (0, 1, 2, 3, 4)
     assert sp.select_dsd_kernel(0) == prev
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0
