@@ -144,3 +144,17 @@ def test_bitmask_bytes(trans):
     rows, cols = (70, 3) if trans else (3, 70)
     words = (cols + 63) // 64
     assert sp.lib().sputnik_bitmask_bytes(ctypes.byref(a._c())) == rows * words * 8
+
+
+def test_dsd4w_asm_matches_generator():
+    """sputnik_amd/csrc/dsd4w_asm.inc is generated by gen_dsd4w.py (the Makefile
+    regenerates it when the generator changes); the committed copy must be
+    exactly the generator's output."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gen = os.path.join(root, "sputnik_amd", "csrc", "gen_dsd4w.py")
+    spec = importlib.util.spec_from_file_location("gen_dsd4w", gen)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with open(os.path.join(root, "sputnik_amd", "csrc", "dsd4w_asm.inc")) as f:
+        assert f.read() == mod.render()
