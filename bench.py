@@ -224,8 +224,14 @@ class DsdProblem:
             meta = (cols // BLOCK + 1) * 4 + self.nb * (2 + 4)
         self.bytes = nz * 2 + meta + k * n * 2 + m * n * 2
         self.dtype_code = 0 if dtype == "f16" else 1
-        self.kernel = (f"block_gemm_kernel<{dtype}, DSD {'T' if ta else 'N'}"
-                       f"{'T' if tb else 'N'}, 128x512 staggered tile>")
+        plan = sp.dsd_plan(self.A, ta, self.B, tb, self.C)
+        tr = f"DSD {'T' if ta else 'N'}{'T' if tb else 'N'}"
+        self.kernel = {
+            1: f"dsd4w_kernel<{dtype}, {tr}, 128x512 tile, 4 waves of 128x128, "
+               f"hand-scheduled k-loop>",
+            2: f"block_gemm_kernel<{dtype}, {tr}, tall 128x256 x2 per CU>",
+            3: f"block_gemm_kernel<{dtype}, {tr}, split mode>",
+        }.get(plan, f"block_gemm_kernel<{dtype}, {tr}, 128x512 staggered tile>")
 
     def launcher(self):
         import torch

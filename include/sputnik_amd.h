@@ -160,6 +160,13 @@ const char *sputnik_build_hash(void);
 int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_block_matrix_t *c);
+/* DSD kernel plan of a problem launched on `stream` (no launch; makes the
+ * launch's workspace decisions): 0 = the 8-wave 128x512 tile, 1 = the
+ * 4-wave hand-scheduled kernel, 2 = the tall configuration, 3 = split mode,
+ * -1 = the problem is rejected. */
+int sputnik_dsd_plan(const sputnik_block_matrix_t *a, int transpose_a,
+                     const sputnik_matrix_t *b, int transpose_b,
+                     const sputnik_matrix_t *c, hipStream_t stream);
 /* Number of pair hand-offs on the current device whose consumer workgroup
  * timed out waiting for its partial (a bounded 0.2 s wait) since the last
  * call; such a consumer's output tile is written as NaN, never as a partial

@@ -141,7 +141,7 @@ def main():
         out[k] = {"us": round(med, 2), "tflops": round(flops / med / 1e6, 1),
                   "min": round(min(ts), 2)}
         if k in stamps:
-            st = sorted(stamps[k])
+            st = sorted(stamps[k], key=lambda x: x[0])
             out[k]["cyc_per_step"] = round(st[len(st) // 2][0], 1)
             out[k]["ghz"] = round(float(np.median([x[1] for x in st])), 3)
             out[k]["timeline"] = {kk: round(float(v), 2) for kk, v in st[len(st) // 2][2].items()}

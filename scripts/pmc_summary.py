@@ -3,7 +3,8 @@
 -> the JSON bench.py reads as roofline.traffic (keyed by shape, density and
 build hash).
 
-Per launch (median over the profiled dispatches of block_gemm_kernel):
+Per launch (median over the profiled dispatches of the DSD kernel,
+block_gemm_kernel or dsd4w_kernel):
   hbm_bytes_per_launch = FETCH_SIZE x 2 + WRITE_SIZE (kilobytes in the CSV).
       MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes
       of a wide (16 B/lane) coalesced read, so it is doubled; WRITE_SIZE is
@@ -48,7 +49,7 @@ def main():
         for f in glob.glob(os.path.join(ddir, "p*", "**", "*counter_collection.csv"),
                            recursive=True):
             for row in csv.DictReader(open(f)):
-                if "block_gemm" not in row["Kernel_Name"]:
+                if not re.search(r"block_gemm_kernel|dsd4w_kernel", row["Kernel_Name"]):
                     continue
                 vals.setdefault(row["Counter_Name"], []).append(
                     float(row["Counter_Value"]))

@@ -4,7 +4,8 @@
 
 bench.py runs the headline density first: its launcher makes one checked
 call, then W warm-up calls, then the K timed calls, so the timed launches
-are block_gemm dispatches [1 + W, 1 + W + K) in start-time order.
+are DSD kernel dispatches (block_gemm_kernel / dsd4w_kernel) [1 + W, 1 + W
++ K) in start-time order.
 Writes a JSON summary (average / median / min / max over the timed calls,
 plus every duration) next to the numbers bench.py reported.
 Usage: trace_headline.py <rocprof out dir> <bench json line file> W K <out.json>
@@ -22,7 +23,8 @@ def main():
     rows = []
     for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "block_gemm_kernel" in r["Kernel_Name"]:
+            if ("block_gemm_kernel" in r["Kernel_Name"]
+                    or "dsd4w_kernel" in r["Kernel_Name"]):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
                              r["Kernel_Name"]))
     rows.sort()

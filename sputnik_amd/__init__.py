@@ -117,6 +117,7 @@ _SIGNATURES = {
     "sputnik_debug_pair_fault": [ctypes.c_int],
     "sputnik_capture_workspaces": [],
     "sputnik_select_dsd_kernel": [ctypes.c_int],
+    "sputnik_dsd_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P],
 }
 _RESTYPES = {
     "sputnik_abi_block_matrix_size": ctypes.c_size_t,
@@ -414,6 +415,19 @@ def can_implement(op: str, a, transpose_a, b, transpose_b, c) -> bool:
         int(bool(transpose_b)), ctypes.byref(cc)))
 
 
+def dsd_plan(a, transpose_a, b, transpose_b, c, stream=None) -> int:
+    """Kernel a DSD launch on `stream` (torch's current stream by default)
+    would use: 0 8-wave tile, 1 4-wave kernel, 2 tall, 3 split, -1 rejected
+    (sputnik_dsd_plan)."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    ca, cb, cc = a._c(), b._c(), c._c()
+    return int(lib().sputnik_dsd_plan(ctypes.byref(ca), int(bool(transpose_a)),
+                                      ctypes.byref(cb), int(bool(transpose_b)),
+                                      ctypes.byref(cc), ctypes.c_void_p(stream)))
+
+
 def select_dsd_kernel(four_wave: int = -1) -> int:
     """DSD NN kernel choice (sputnik_select_dsd_kernel): 1 the 4-wave
     hand-scheduled kernel where it pays (default), 2 wherever it applies, 0
@@ -435,7 +449,7 @@ __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
     "build_hash", "capture_workspaces", "pair_errors", "sdd_plan",
-    "select_dsd_kernel",
+    "select_dsd_kernel", "dsd_plan",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",

@@ -52,6 +52,10 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 // k-split 128x128 block per workgroup, -1 = rejected. Reads the CU count of
 // the current device (no launch).
 int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
+// DSD kernel plan (dispatch.cpp DsdPlan): 0 8-wave tile, 1 4-wave kernel,
+// 2 tall, 3 split mode, -1 rejected.
+int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
+            hipStream_t stream);
 
 // Pair hand-offs that timed out (see dispatch.cpp), and the test knob that
 // makes every pair producer skip its publish.

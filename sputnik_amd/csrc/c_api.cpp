@@ -263,6 +263,16 @@ int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                               &cc);
 }
 
+int sputnik_dsd_plan(const sputnik_block_matrix_t *a, int transpose_a,
+                     const sputnik_matrix_t *b, int transpose_b,
+                     const sputnik_matrix_t *c, hipStream_t stream) {
+  if (!a || !b || !c) return -1;
+  const BlockMatrix ca = ToCpp(a);
+  const Matrix cb = ToCpp(b), cc = ToCpp(c);
+  return sputnik_amd::DsdPlan(&ca, transpose_a != 0, &cb, transpose_b != 0, &cc,
+                              stream);
+}
+
 int sputnik_pair_errors(void) { return sputnik_amd::PairErrors(); }
 
 void sputnik_debug_pair_fault(int on) { sputnik_amd::SetPairFault(on); }

@@ -1191,6 +1191,31 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
   return UseGroupedSdd(&p, cm, tb) ? 1 : 0;
 }
 
+// Which kernel RunDsd would launch for this problem on `stream` (no
+// launch): 0 the 8-wave 128 x 512 tile, 1 the 4-wave hand-scheduled kernel
+// (dsd4w.hip), 2 the tall configuration, 3 split mode, -1 rejected. Makes
+// the same workspace decisions a launch would (pair workspace, tile
+// counter), so it may allocate them.
+int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
+            hipStream_t stream) {
+  if (!a || !b || !c) return -1;
+  GemmParams p;
+  bool needs_meta = false;
+  const BlockMatrix &am = *static_cast<const BlockMatrix *>(a);
+  if (PrepareDsd(am, ta, *static_cast<const Matrix *>(b), tb,
+                 *static_cast<const Matrix *>(c), &p, &needs_meta) != Status::kOk)
+    return -1;
+  PreparePairs(&p, am.nonzeros / (kBlock * kBlock), stream);
+  const bool tall = UseTall(&p, stream);
+  if (Dsd4wEnabled() &&
+      Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : am.nonzeros / (kBlock * kBlock),
+                   !ta, tb, false, tall))
+    return 1;
+  if (tall) return 2;
+  if (p.pair != 0 && p.pair_split > 1) return 3;
+  return 0;
+}
+
 // Host-only acceptance test (no launch, no device needed): op 0 = DSD
 // (a: block, b/c: dense), 1 = DDS (b: block), 2 = SDD (c: block), 3 = SSD
 // (a, c: block), 4 = SDS (b, c: block), 5 = DSS (a, b: block). The C

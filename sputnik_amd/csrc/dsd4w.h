@@ -13,9 +13,9 @@ namespace sputnik_amd {
 // straight output, on the one-tile-per-CU 128 x 512 launch (plain or pair
 // balanced; not split mode, not persistent, not the tall configuration).
 // blocks: stored blocks of the sparse operand; below a mean of
-// kDsd4wMinMean blocks per block-row the 8-wave kernel is faster (its fixed
-// per-tile costs are shared by twice the waves; r04 A/B).
-constexpr int kDsd4wMinMean = 12;
+// kDsd4wMinMean blocks per block-row (where pair balancing is off too) the
+// 8-wave kernel keeps the launch (not measured against it there).
+constexpr int kDsd4wMinMean = 2;
 bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
                   bool out_t, bool tall);
 
@@ -26,7 +26,11 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 // same with the last block specialized (no dummy DMA / reads, conversion
 // inside the final step's MFMAs).
 hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
-constexpr int kDsd4wDefaultEpi = 0;
+// The per-wave epilogue: DSD 4096^3 same-process A/B (r04b, us) 8-wave /
+// 4-wave workgroup epilogue / per-wave: 50% 63.5 / 61.2 / 60.6, 10% 27.4 /
+// 28.4 / 27.1, 30% 43.7 / 45.2 / 43.7, 90% 97.7 / 93.9 / 93.0; the
+// specialized last block (2) tied with it (60.8 / 27.2 / 43.7 / 93.1).
+constexpr int kDsd4wDefaultEpi = 1;
 
 }  // namespace sputnik_amd
 
