@@ -7,7 +7,7 @@ mkdir -p $ROOT/build/exp
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   d=$ROOT/build/exp/$name; mkdir -p $d
-  for f in block_gemm metadata dispatch c_api; do
+  for f in block_gemm dsd4w metadata dispatch c_api; do
     src=$ROOT/sputnik_amd/csrc/$f.hip; [ -f $src ] || src=$ROOT/sputnik_amd/csrc/$f.cpp
     /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC --offload-arch=gfx950 -I$ROOT/include $flags -x hip -c $src -o $d/$f.o &
     pids="$pids $!"

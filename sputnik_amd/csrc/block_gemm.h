@@ -1587,7 +1587,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         if (xcd2) {
           const int x = b & 7, k = b >> 3;
           panel = 2 * (x >> 1) + (k & 1);
-          pi = (x & 1) * (half >> 1) + (k >> 1);
+          pi = p.pair_xcd2 == 2 ? 2 * (k >> 1) + (x & 1)
+                                  : (x & 1) * (half >> 1) + (k >> 1);
         } else {
           const int t = xcd_tile(b, n_light);
           panel = t / half;

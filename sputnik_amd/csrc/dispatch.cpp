@@ -301,7 +301,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     const char *e = std::getenv("SPUTNIK_AMD_PAIR_XCD2");
     return e != nullptr ? std::atoi(e) : SPUTNIK_PAIR_XCD2_DEFAULT;
   }();
-  p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? 1 : 0;
+  p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? xcd2 : 0;
   // Split mode (GemmParams::pair_split) when the tiles fill at most half of
   // the workgroup slots (e.g. 512-2048-row panels of a strong-scaled 4096^2,
   // or narrow N) and the rows hold at least 4 blocks on average: two

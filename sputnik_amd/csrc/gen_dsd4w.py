@@ -213,13 +213,19 @@ def prologue():
             "s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
             "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
-    for slot in range(3):
+    # steps 0 and 1, wait for step 0 only, then step 2's DMA issued behind
+    # the step-0 fragment reads: the CU's TA serializes the 30 DMAs of every
+    # wave, and only step 0 is needed before the first MFMA
+    for slot in range(2):
         for m0, ld in dmas(slot):
             out += [m0, "s_nop 0", ld]
         out += ADVANCE
     # (no accumulator zeroing: the first step's MFMAs take C = 0)
-    out += ["s_waitcnt vmcnt(20)", "s_barrier"]
+    out += ["s_waitcnt vmcnt(10)", "s_barrier"]
     out += d_reads(0, 0) + s_reads(0, 0)
+    for m0, ld in dmas(2):
+        out += [m0, "s_nop 0", ld]
+    out += ADVANCE
     out.append("s_waitcnt lgkmcnt(0)")
     return out
 
@@ -347,9 +353,14 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt, wave_epi=False, last_block=False):
+def build(dt, wave_epi=False, last_block=False, stamps=False):
+    """stamps (experiment builds, SPUTNIK_EXP & 512): s_memrealtime into the
+    outputs %[r0] (k-loop start), %[r1] (k-loop end), %[r2] (body end), %[r3]
+    and %[r4] (a producer's publish start and end)."""
     cvt = f"v_cvt_pk_{dt}_f32"
     body = prologue()
+    if stamps:
+        body.append("s_memrealtime %[r0]")
     # the first block's step 0 is the zero-C copy below (L_first)
     body.append("s_branch L_first_%=")
     body.append("L_loop_%=:")
@@ -369,13 +380,19 @@ def build(dt, wave_epi=False, last_block=False):
              "s_branch L_exit_%="]
     if last_block:
         body.append("L_last_%=:")
+        if stamps:
+            body.append("s_memrealtime %[r1]")
         body += step(dt, 0)
         for H in (1, 2, 3):
             body += step(dt, H, last=H, cvt=cvt)
         body += ["s_nop 7", "s_nop 7"] + convert(cvt, 62) + convert(cvt, 63)
         body.append("s_branch L_done_%=")
     body.append("L_pub_%=:")
+    if stamps:
+        body += ["s_memrealtime %[r3]", "s_waitcnt lgkmcnt(0)"]
     body += publish()
+    if stamps:
+        body += ["s_memrealtime %[r4]", "s_waitcnt lgkmcnt(0)"]
     body += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_zero_%="]
     # step 0 of a block with the accumulators restarting from zero (C = 0):
     # the launch's first step, and the first step after a pair publish
@@ -385,6 +402,8 @@ def build(dt, wave_epi=False, last_block=False):
     body.append("L_zero_%=:")
     body += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
     body.append("L_exit_%=:")
+    if stamps:
+        body.append("s_memrealtime %[r1]")
     if wave_epi:
         # the wave's own DMAs (the loop's last three steps fed clamped
         # dummies) landed and its reads are done: its D ring region is free
@@ -406,6 +425,8 @@ def build(dt, wave_epi=False, last_block=False):
     body += epilogue_body(cvt, "nan", wave_epi)
     body += ["L_done_%=:"]
     body += copy_out() if wave_epi else ["s_waitcnt lgkmcnt(0)"]
+    if stamps:
+        body += ["s_memrealtime %[r2]", "s_waitcnt lgkmcnt(0)"]
     return body
 
 
@@ -418,6 +439,10 @@ def render():
             lines.append(f"#define {name} \\")
             lines += [f'  "{ins}\\n" \\' for ins in build(dt, wave_epi, last_block)]
             lines += ['  ""', ""]
+        # the default epilogue with timeline stamps (experiment builds)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_T \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, True)]
+        lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]
             + [f'"s{i}"' for i in range(84, 88)] + [f'"s{i}"' for i in range(96, 100)]
