@@ -98,6 +98,10 @@ def main():
                      "end_max": round(float(us(t[xcd == x, 4].max() - e0)), 2),
                      "loop_start_max": round(float(us(t[xcd == x, 2].max() - e0)), 2)}
             for x in range(8) if (xcd == x).any()}
+        # the 12 latest-ending workgroups: end, role, blocks, first segment, XCD share
+        order = np.argsort(-t[:, 4])[:12]
+        out["latest"] = [[round(us(t[i, 4] - e0), 2), int(t[i, 6]), int(t[i, 5]),
+                          int(t[i, 8]), int(xcd[i])] for i in order]
         print(json.dumps(out), flush=True)
 
 

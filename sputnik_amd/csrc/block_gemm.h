@@ -177,7 +177,8 @@ struct GemmParams {
   // Pair launches with 8 panels: XCD x (= workgroup b mod 8) takes panels
   // 2(x/2) and 2(x/2)+1 for half of the pairs instead of one panel for all
   // of them, so it streams half of S (each block used by two tiles) and
-  // two D panels (host: dispatch.cpp PreparePairs).
+  // two D panels (host: dispatch.cpp PreparePairs). 0 off; 1 / 3 which
+  // XCD of a panel pair takes the heavy half of the pairs; 2 interleaved.
   int pair_xcd2;
   // Split mode (pair_split = 2; at most half as many tiles as CUs, e.g. the
   // 512 to 2048-row panels of a strong-scaled 4096^2): grid = 2 x
@@ -1578,7 +1579,8 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       int role, panel, pi;  // role 0 light, 1 middle, 2 heavy; pi = pair
       // GemmParams::pair_xcd2 (8 panels, no middle row, an even number of
       // pairs): XCD x = b mod 8 takes panels 2(x/2), 2(x/2)+1 and pairs
-      // [(x mod 2) half/2, +half/2). A bijection on each role's (panel,
+      // [(x mod 2) half/2, +half/2) (mode 1), [(1 - x mod 2) half/2, ..)
+      // (mode 3) or x mod 2, + 2, .. (mode 2). A bijection on each role's (panel,
       // pair), so producers still precede their consumers.
       // (DSD only: measured there.)
       const bool xcd2 = !kOutT && p.pair_xcd2 != 0 && p.num_jtiles == 8 &&
@@ -1588,7 +1590,7 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
           const int x = b & 7, k = b >> 3;
           panel = 2 * (x >> 1) + (k & 1);
           pi = p.pair_xcd2 == 2 ? 2 * (k >> 1) + (x & 1)
-                                  : (x & 1) * (half >> 1) + (k >> 1);
+             : ((x & 1) ^ (p.pair_xcd2 == 3 ? 1 : 0)) * (half >> 1) + (k >> 1);
         } else {
           const int t = xcd_tile(b, n_light);
           panel = t / half;

@@ -220,7 +220,7 @@ static bool PairsEnabled() {
 #define SPUTNIK_PAIR_MIN_MEAN4 8  // 4 x mean blocks per row
 #endif
 #ifndef SPUTNIK_PAIR_XCD2_DEFAULT
-#define SPUTNIK_PAIR_XCD2_DEFAULT 1
+#define SPUTNIK_PAIR_XCD2_DEFAULT 3
 #endif
 static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair = 0;
@@ -296,7 +296,14 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   p->pair_fault = g_pair_fault;
   // Two panels x half the pairs per XCD (GemmParams::pair_xcd2) from a mean
   // of 8 blocks per row: DSD 4096^3 A/B (r02m) 30% / 50% / 90% +1.2 / +2.7
-  // / +2.8%, 10% -4.4%. SPUTNIK_AMD_PAIR_XCD2=0 turns it off.
+  // / +2.8%, 10% -4.4%. SPUTNIK_AMD_PAIR_XCD2=0 turns it off. Mode 3 (the
+  // default) gives the heavy half of the pairs (the ones with hand-offs) to
+  // the odd XCD of each panel pair: per-workgroup timelines (r04f/g,
+  // scripts/exp_timeline4w.py) show logical XCDs 0/2/4/6 running the same
+  // k-loop ~6% slower per block than 1/3/7 on every box measured, and mode
+  // 1 had put the critical pairs exactly there (4-wave A/B, separate
+  // processes, 30/50/90%: +1.0/+2.1/+1.4%, 10% +0.5%). Mode 2 interleaves
+  // the pairs (r04d: +0.5% at 50%).
   static const int xcd2 = [] {
     const char *e = std::getenv("SPUTNIK_AMD_PAIR_XCD2");
     return e != nullptr ? std::atoi(e) : SPUTNIK_PAIR_XCD2_DEFAULT;
