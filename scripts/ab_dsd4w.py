@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--calls", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--dim", type=int, default=4096)
+    ap.add_argument("--op", default="dsd", choices=["dsd", "dds"],
+                    help="dds: bench.py's OpProblem DDS NN (the kDds kernel)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -34,7 +36,12 @@ def main():
         rng = np.random.default_rng(1)
         nz = mu.nonzeros_for_density(d, d, dens)
         off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
-        prob = bench.DsdProblem(d, d, off, idx, d, False, False, a.dtype, 7, dev)
+        if a.op == "dds":
+            ns = argparse.Namespace(op="dds", trans="NN", api="ex", k=d,
+                                    density=dens, dtype=a.dtype, seed=0)
+            prob = bench.OpProblem(ns, dev)
+        else:
+            prob = bench.DsdProblem(d, d, off, idx, d, False, False, a.dtype, 7, dev)
         fn = prob.launcher()
 
         def timed(four):
@@ -60,7 +67,7 @@ def main():
                 ts[k].append(timed(mode))
         sp.select_dsd_kernel(1)
         med = lambda v: sorted(v)[len(v) // 2]
-        out = {"density": dens, "dtype": a.dtype, "dim": d}
+        out = {"op": a.op, "density": dens, "dtype": a.dtype, "dim": d}
         for k, v in ts.items():
             out[k] = {"us": round(med(v), 2),
                       "tflops": round(prob.flops / med(v) / 1e6, 1),

@@ -550,6 +550,7 @@ Status PrepareDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   p->d_ld = (long long)s.lda * 2;
   p->c_data = static_cast<char *>(c.data);
   p->c_ld = (long long)s.ldc * 2;
+  p->s_blocks = (int)(b.nonzeros / (kBlock * kBlock));
   p->num_rows = s.n / kBM;
   p->num_jtiles = (s.m + CfgSparse::kBN - 1) / CfgSparse::kBN;
   p->j_limit = s.m;
@@ -911,6 +912,17 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   p.debug = g_debug;
   PreparePairs(&p, b.nonzeros / (kBlock * kBlock), stream);
   const bool tall = UseTall(&p, stream);
+  if (Dsd4wEnabled() &&
+      Dds4wApplies(p, Dsd4wForced() ? (1LL << 40) : b.nonzeros / (kBlock * kBlock),
+                   tb, !ta, true, tall)) {
+    // (the two-panel pair placement: DSD-measured; DDS experiment knob)
+    static const int dds_xcd2 = [] {
+      const char *e = std::getenv("SPUTNIK_AMD_DDS_XCD2");
+      return e != nullptr ? std::atoi(e) : 0;
+    }();
+    if (p.pair_xcd2 != 0) p.pair_xcd2 = dds_xcd2;
+    return LaunchDds4w(dtype, p, stream);
+  }
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);
 }

@@ -32,6 +32,13 @@ hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, hipStream_t stre
 // specialized last block (2) tied with it (60.8 / 27.2 / 43.7 / 93.1).
 constexpr int kDsd4wDefaultEpi = 1;
 
+// DDS NN (op(B)^T rows = B's block-columns through its transposed metadata,
+// A k-contiguous, transposed output) on the same kernel with the operand
+// images swapped (dsd4w.hip kDds), per-wave epilogue; M a multiple of 128.
+bool Dds4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
+                  bool out_t, bool tall);
+hipError_t LaunchDds4w(int dtype, const GemmParams &p, hipStream_t stream);
+
 }  // namespace sputnik_amd
 
 #endif  // SPUTNIK_AMD_DSD4W_H_

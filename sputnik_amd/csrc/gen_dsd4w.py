@@ -58,9 +58,7 @@ FS = (128, 192)
 FD = (160, 224)
 SLOT = 8192
 DMA_POS = [3, 9, 15, 21, 27, 33, 39, 45, 51, 57]
-D_READS_AT = 2
-BARRIER_AT = 18
-S_READS_AT = 19
+READS_AT = 2    # own image's reads from here, then the barrier, then the shared image's
 NAN_F16 = "0x7e007e00"
 NAN_BF16 = "0x7fc07fc0"
 WAIT_TICKS = 20000000   # s_memrealtime (100 MHz): 0.2 s (block_gemm.h kPairWaitTicks)
@@ -107,8 +105,16 @@ def dmas(slot):
 
 # The fed block advances one k-step: S by 64 B (32 k of a 256-B row), D by
 # 32 rows.
-ADVANCE = ["s_add_u32 s40, s40, 64", "s_addc_u32 s41, s41, 0",
-           "s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
+# DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
+# [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
+# the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
+VARIANT = {"dds": False}
+
+
+def advance():
+    s = 8192 if VARIANT["dds"] else 64
+    return [f"s_add_u32 s40, s40, {s}", "s_addc_u32 s41, s41, 0",
+            "s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
 
 
 def entry_of(xreg, out_reg):
@@ -122,22 +128,34 @@ def entry_of(xreg, out_reg):
 # last): S block = its entry (storage order), D rows = 128 x its k-block
 # (s58, loaded a block ahead); then s58 <- the k-block the index prefetch
 # brought in (s59 >> s60).
-SWITCH = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
-          + entry_of("s57", "s76")
-          + ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15",
-             "s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
-             "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
-             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
-             "s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"])
+# (DDS: the S block is the storage block of the entry, s_block_offsets[e],
+# kept in s63 and prefetched into s62 like the k-block.)
+def switch():
+    if VARIANT["dds"]:
+        blk = ["s_lshr_b32 s77, s63, 17", "s_lshl_b32 s76, s63, 15"]
+    else:
+        blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
+               + entry_of("s57", "s76")
+               + ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15"])
+    out = blk + ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
+                 "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
+                 "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
+                 "s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"]
+    if VARIANT["dds"]:
+        out.append("s_mov_b32 s63, s62")
+    return out
 
 # Scalar load of the k-block (int16) of virtual entry min(s56, xlast) into
 # s59 (its half in s60), one block ahead of the SWITCH that uses it.
-IDX_LOAD = (["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"]
-            + entry_of("s78", "s79")
-            + ["s_lshl_b32 s79, s79, 1", "s_and_b32 s60, s79, 2",
-               "s_lshl_b32 s60, s60, 3", "s_and_b32 s79, s79, 0xfffffffc",
-               "s_add_u32 s76, %[ixlo], s79", "s_addc_u32 s77, %[ixhi], 0",
-               "s_load_dword s59, s[76:77], 0x0"])
+def idx_load():
+    out = ["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"] + entry_of("s78", "s79")
+    if VARIANT["dds"]:
+        out += ["s_lshl_b32 s74, s79, 2", "s_add_u32 s74, %[bolo], s74",
+                "s_addc_u32 s75, %[bohi], 0", "s_load_dword s62, s[74:75], 0x0"]
+    return out + ["s_lshl_b32 s79, s79, 1", "s_and_b32 s60, s79, 2",
+                  "s_lshl_b32 s60, s60, 3", "s_and_b32 s79, s79, 0xfffffffc",
+                  "s_add_u32 s76, %[ixlo], s79", "s_addc_u32 s77, %[ixhi], 0",
+                  "s_load_dword s59, s[76:77], 0x0"]
 
 
 def step(dt, H, zero_c=False, last=0, cvt=None):
@@ -154,27 +172,32 @@ def step(dt, H, zero_c=False, last=0, cvt=None):
     cur, nxt = H % 2, 1 - H % 2
     gaps = [[] for _ in range(64)]
     if H == 0:
-        gaps[0] += IDX_LOAD
+        gaps[0] += idx_load()
     if last != 3:
         # own DMA of step + 1 landed (step + 2's 10 may still fly)
         gaps[1].append("s_waitcnt vmcnt(0)" if last == 2 else "s_waitcnt vmcnt(10)")
     if H == 1 and not last:
-        gaps[1] += SWITCH
+        gaps[1] += switch()
     if last != 3:
-        for i, ins in enumerate(d_reads((H + 1) % 4, nxt)):
-            gaps[D_READS_AT + i].append(ins)
+        # the wave's own image first, then (after the barrier) the shared one:
+        # DSD D (tr) / S (b128), DDS the other way round
+        own, shared = d_reads((H + 1) % 4, nxt), s_reads((H + 1) % 4, nxt)
+        if VARIANT["dds"]:
+            own, shared = shared, own
+        for i, ins in enumerate(own):
+            gaps[READS_AT + i].append(ins)
         # every wave's S DMA of step + 1 landed (each waited above) / every
         # wave done reading the slot refilled below (its reads were waited at
         # the end of step - 2)
-        gaps[BARRIER_AT].append("s_barrier")
-        for i, ins in enumerate(s_reads((H + 1) % 4, nxt)):
-            gaps[S_READS_AT + i].append(ins)
+        gaps[READS_AT + len(own)].append("s_barrier")
+        for i, ins in enumerate(shared):
+            gaps[READS_AT + len(own) + 1 + i].append(ins)
     if not last:
         for (m0, ld), k in zip(dmas((H + 3) % 4), DMA_POS):
             gaps[k - 1].append(m0)
             gaps[k].append(ld)
         if H != 0:
-            gaps[58] += ADVANCE
+            gaps[58] += advance()
     if last == 3:
         for i in range(2, 64):
             gaps[i] += convert(cvt, i - 2)
@@ -205,12 +228,17 @@ def prologue():
            "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
            "s_mov_b32 s56, 2", "s_mov_b32 s57, 0",
            "s_mov_b32 s58, %[kb1]", "s_mov_b32 s61, %[ntot]",
-           "s_mov_b32 s72, 4096", "s_mov_b32 s64, 0"]
+           f"s_mov_b32 s72, {1024 if VARIANT['dds'] else 4096}", "s_mov_b32 s64, 0"]
     out += [f"s_mul_i32 s{64 + q}, %[k4], {q}" for q in range(1, 8)]
-    # block 0: virtual entry 0, k-block kb0
-    out += entry_of("s57", "s76")
-    out += ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15",
-            "s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
+    # block 0: virtual entry 0, k-block kb0 (DDS: storage block bo0; s63 =
+    # entry 1's, bo1)
+    if VARIANT["dds"]:
+        out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
+                "s_mov_b32 s63, %[bo1]"]
+    else:
+        out += entry_of("s57", "s76")
+        out += ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15"]
+    out += ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
             "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
     # steps 0 and 1, wait for step 0 only, then step 2's DMA issued behind
@@ -219,13 +247,13 @@ def prologue():
     for slot in range(2):
         for m0, ld in dmas(slot):
             out += [m0, "s_nop 0", ld]
-        out += ADVANCE
+        out += advance()
     # (no accumulator zeroing: the first step's MFMAs take C = 0)
     out += ["s_waitcnt vmcnt(10)", "s_barrier"]
     out += d_reads(0, 0) + s_reads(0, 0)
     for m0, ld in dmas(2):
         out += [m0, "s_nop 0", ld]
-    out += ADVANCE
+    out += advance()
     out.append("s_waitcnt lgkmcnt(0)")
     return out
 
@@ -353,7 +381,15 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt, wave_epi=False, last_block=False, stamps=False):
+def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False):
+    VARIANT["dds"] = dds
+    try:
+        return _build(dt, wave_epi, last_block, stamps)
+    finally:
+        VARIANT["dds"] = False
+
+
+def _build(dt, wave_epi, last_block, stamps):
     """stamps (experiment builds, SPUTNIK_EXP & 512): s_memrealtime into the
     outputs %[r0] (k-loop start), %[r1] (k-loop end), %[r2] (body end), %[r3]
     and %[r4] (a producer's publish start and end)."""
@@ -442,6 +478,10 @@ def render():
         # the default epilogue with timeline stamps (experiment builds)
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_T \\")
         lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, True)]
+        lines += ['  ""', ""]
+        # DDS NN (dds4w, the same kernel with the operand images swapped)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_DDS \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, True)]
         lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

@@ -119,3 +119,94 @@ def test_dsd4w_selector_roundtrip():
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0
     assert sp.select_dsd_kernel(-1) == prev
+
+
+# ------------------------------------------------------------------ DDS NN --
+# The same kernel with the operand images swapped (dsd4w.hip kDds): C = A . B
+# with B sparse in column order (its transposed metadata), against the
+# 8-wave kernel's kOutT path (same k order and MFMA operand roles, so again
+# torch.equal) and the oracle.
+
+def _dds_problem(m, k, n, density, dtype, seed, empty_cols=()):
+    rng = np.random.default_rng(seed)
+    R, C = k // 128, n // 128
+    nz = mu.nonzeros_for_density(k, n, density) // (128 * 128)
+    off, idx = mu.random_topology(R, C, nz, rng, unordered=True)
+    if empty_cols:
+        rows = np.repeat(np.arange(R), np.diff(off))
+        keep = ~np.isin(idx, empty_cols)
+        rows, idx = rows[keep], idx[keep]
+        off = np.zeros(R + 1, np.int32)
+        np.cumsum(np.bincount(rows, minlength=R), out=off[1:])
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    nb = int(off[-1])
+    a = (torch.rand(m * k, generator=g, device="cuda") * 2 - 1).to(td)
+    b = (torch.rand(max(nb, 1) * 16384, generator=g, device="cuda") * 2 - 1).to(td)
+    B = sp.BlockMatrix(k, n, 128, nb * 16384, b,
+                       torch.from_numpy(np.asarray(off, np.int32)).cuda(),
+                       torch.from_numpy(np.asarray(idx).astype(np.int16)).cuda())
+    sp.AllocateTransposeBuffers(B)
+    sp.Transpose(B)
+    return sp.Matrix(m, k, a), B, off, idx, a, b
+
+
+def _run_dds(A, B, m, n, dtype, mode):
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+    prev = sp.select_dsd_kernel(mode)
+    try:
+        sp.MatmulEx(A, False, B, False, sp.Matrix(m, n, c))
+        torch.cuda.synchronize()
+    finally:
+        sp.select_dsd_kernel(prev)
+    return c.view(m, n)
+
+
+DDS_CASES = [
+    # m, k, n, density
+    (4096, 4096, 4096, 0.2),    # BASELINE config 3's DDS
+    (4096, 4096, 4096, 0.5),
+    (4096, 4096, 4096, 0.05),
+    (4096, 4096, 4096, 0.9),
+    (2048, 4096, 4096, 0.3),    # 4 row panels
+    (1152, 2048, 2048, 0.5),    # last tile: one wave block inside M, three past it
+    (4096, 2048, 8192, 0.3),    # 64 block-columns: workgroup ranking
+    (4096, 4096, 1024, 0.5),    # 8 block-columns
+]
+
+
+@pytest.mark.parametrize("m,k,n,density", DDS_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dds4w_bit_identical_to_8wave(m, k, n, density, dtype):
+    A, B, off, idx, a, b = _dds_problem(m, k, n, density, dtype,
+                                        seed=m + 3 * n + int(density * 100))
+    c4 = _run_dds(A, B, m, n, dtype, 3)
+    c8 = _run_dds(A, B, m, n, dtype, 0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+
+
+def test_dds4w_empty_columns_and_oracle():
+    m, k, n = 1536, 2048, 4096
+    A, B, off, idx, a, b = _dds_problem(m, k, n, 0.5, "f16", seed=5,
+                                        empty_cols=(0, 7, 31))
+    c4 = _run_dds(A, B, m, n, "f16", 3)
+    c8 = _run_dds(A, B, m, n, "f16", 0)
+    assert torch.equal(c4, c8)
+    for c in (0, 7, 31):
+        assert torch.count_nonzero(c4[:, c * 128:(c + 1) * 128]) == 0
+    av = a.float().cpu().numpy().reshape(m, k)
+    bv = b.float().cpu().numpy().reshape(-1, 128, 128)
+    for c in (1, 17, 30):
+        col = np.zeros((k, 128), np.float32)
+        for e in range(int(off[-1])):
+            if idx[e] == c:
+                r = int(np.searchsorted(off, e, side="right") - 1)
+                col[r * 128:(r + 1) * 128] = bv[e]
+        ref = O.gemm(av, False, col, False, threads=H.oracle_threads())
+        H.assert_close(c4[:, c * 128:(c + 1) * 128].float().cpu().numpy(), ref,
+                       "f16", f"dds4w block-column {c}")
