@@ -184,11 +184,12 @@ void sputnik_debug_pair_fault(int on);
  * concurrently with a second instantiation of the same capture. Host-only
  * query. */
 int sputnik_capture_workspaces(void);
-/* DSD NN kernel choice (tests and same-process A/B): 1 = the 4-wave
- * hand-scheduled kernel where it applies and pays (the default; environment
- * SPUTNIK_AMD_DSD4W=0 turns it off), 2 / 3 / 4 = wherever it applies,
- * whatever the density, with its workgroup / per-wave / per-wave +
- * specialized-last-block epilogue, 0 = the 8-wave kernel everywhere, -1 =
+/* DSD NN / DDS NN kernel choice (tests and same-process A/B): 1 = the
+ * 4-wave hand-scheduled kernel where it applies and pays (the default;
+ * environment SPUTNIK_AMD_DSD4W=0 turns it off), 2 / 3 / 4 / 5 = wherever it
+ * applies, whatever the density, with its workgroup / per-wave / per-wave +
+ * specialized-last-block / per-wave + double-slot k-contiguous image
+ * variant (DDS: 3 for 2 and 4), 0 = the 8-wave kernel everywhere, -1 =
  * query only. Returns the previous choice. Process-wide. */
 int sputnik_select_dsd_kernel(int four_wave);
 

@@ -55,7 +55,7 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(e) * 1e3 / a.calls
 
-        arms = {"8wave": 0, "4wave": 3, "4wave_lastblk": 4}
+        arms = {"8wave": 0, "4wave": 3, "4wave_ds": 5}
         for mode in arms.values():
             timed(mode)
             for _ in range(100):

@@ -46,7 +46,8 @@ def main():
     res = {"label": label, "build_hash": build, "kernels": {}}
     for k, d in per.items():
         v, dur = d["vals"], median(d["durs"])
-        e = {"profiled_kernel_us": round(dur * 1e6, 2), "dispatches": len(d["durs"])}
+        e = {"profiled_kernel_us": round(dur * 1e6, 2), "dispatches": len(d["durs"]),
+             "counters": {c: median(x) for c, x in sorted(v.items())}}
         if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
             fetch = median(v["FETCH_SIZE"]) * 1024 * 2
             write = median(v["WRITE_SIZE"]) * 1024

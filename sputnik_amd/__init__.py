@@ -429,9 +429,10 @@ def dsd_plan(a, transpose_a, b, transpose_b, c, stream=None) -> int:
 
 
 def select_dsd_kernel(four_wave: int = -1) -> int:
-    """DSD NN kernel choice (sputnik_select_dsd_kernel): 1 the 4-wave
-    hand-scheduled kernel where it pays (default), 2 wherever it applies, 0
-    the 8-wave kernel, -1 query only. Returns the previous choice."""
+    """DSD NN / DDS NN kernel choice (sputnik_select_dsd_kernel): 1 the
+    4-wave hand-scheduled kernel where it pays (default), 2-5 wherever it
+    applies (its epilogue / double-slot variants), 0 the 8-wave kernel, -1
+    query only. Returns the previous choice."""
     return int(lib().sputnik_select_dsd_kernel(int(four_wave)))
 
 

@@ -391,14 +391,14 @@ static int Dsd4wMode() {
   if (v < 0) {
     const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
     v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 4 ? 4 : v);
+    v = v < 0 ? 1 : (v > 5 ? 5 : v);
     g_dsd4w.store(v, std::memory_order_relaxed);
   }
   return v;
 }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2..4: wherever the kernel can run, whatever the density (tests, A/B), with
-// epilogue 0 / 1 / 2 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
+// 2..5: wherever the kernel can run, whatever the density (tests, A/B), with
+// epilogue 0 / 1 / 2 / 3 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
 bool Dsd4wForced() { return Dsd4wMode() >= 2; }
 int Dsd4wEpi() {
   const int m = Dsd4wMode();
@@ -407,7 +407,7 @@ int Dsd4wEpi() {
 int SelectDsdKernel(int four_wave) {
   const int prev = Dsd4wMode();
   if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 4 ? 4 : four_wave, std::memory_order_relaxed);
+    g_dsd4w.store(four_wave > 5 ? 5 : four_wave, std::memory_order_relaxed);
   return prev;
 }
 
@@ -921,7 +921,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
       return e != nullptr ? std::atoi(e) : 0;
     }();
     if (p.pair_xcd2 != 0) p.pair_xcd2 = dds_xcd2;
-    return LaunchDds4w(dtype, p, stream);
+    return LaunchDds4w(dtype, p, Dsd4wEpi(), stream);
   }
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);

@@ -24,20 +24,25 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 // epi: 0 one workgroup-wide staging image copied out after a barrier; 1
 // every wave stages and stores its own 128 x 128 block (no barrier); 2 the
 // same with the last block specialized (no dummy DMA / reads, conversion
-// inside the final step's MFMAs).
+// inside the final step's MFMAs); 3 the per-wave epilogue with the
+// k-contiguous image in double slots of 128-B row pieces (gen_dsd4w.py).
 hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
 // The per-wave epilogue: DSD 4096^3 same-process A/B (r04b, us) 8-wave /
 // 4-wave workgroup epilogue / per-wave: 50% 63.5 / 61.2 / 60.6, 10% 27.4 /
 // 28.4 / 27.1, 30% 43.7 / 45.2 / 43.7, 90% 97.7 / 93.9 / 93.0; the
 // specialized last block (2) tied with it (60.8 / 27.2 / 43.7 / 93.1).
-constexpr int kDsd4wDefaultEpi = 1;
+// Double slots (3, the default since r04m): 8-wave / per-wave / double-slot
+// DSD 50% 63.3 / 59.2 / 58.2, 10% 27.4 / 25.5 / 24.9, 30% 43.3 / 40.7 /
+// 40.8, 90% 98.7 / 92.3 / 91.3; DDS 20% 36.0 / 34.6 / 33.0, 50% 67.5 /
+// 64.8 / 60.5, 10% 26.5 / 24.2 / 23.8, 90% 107.7 / 104.2 / 96.0.
+constexpr int kDsd4wDefaultEpi = 3;
 
 // DDS NN (op(B)^T rows = B's block-columns through its transposed metadata,
 // A k-contiguous, transposed output) on the same kernel with the operand
 // images swapped (dsd4w.hip kDds), per-wave epilogue; M a multiple of 128.
 bool Dds4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
                   bool out_t, bool tall);
-hipError_t LaunchDds4w(int dtype, const GemmParams &p, hipStream_t stream);
+hipError_t LaunchDds4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
 
 }  // namespace sputnik_amd
 

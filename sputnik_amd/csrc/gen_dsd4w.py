@@ -108,7 +108,7 @@ def dmas(slot):
 # DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
-VARIANT = {"dds": False}
+VARIANT = {"dds": False, "ds": False}
 
 
 def advance():
@@ -159,6 +159,9 @@ def idx_load():
 
 
 def step(dt, H, zero_c=False, last=0, cvt=None):
+    if VARIANT["ds"]:
+        assert not last
+        return step_ds(dt, H, zero_c)
     """Step H of a block: MFMAs on set H % 2; reads of step + 1 from slot
     (H + 1) % 4 into the other set; DMA of step + 3 into slot (H + 3) % 4
     (H = 0: the fed block's last step; H = 1..3: steps 0..2 of the next
@@ -210,6 +213,145 @@ def step(dt, H, zero_c=False, last=0, cvt=None):
     return out
 
 
+# ---- double-slot mode (VARIANT["ds"]) -----------------------------------
+# The k-contiguous image (DSD: the shared S image, rows of the stored block;
+# DDS: each wave's rows of A) is loaded as 128-byte row pieces covering two
+# k-steps at once: a 128-B piece is a whole cache line, where the 64-B piece
+# of a 32-deep step is half of one and the L1 (32 KiB, refilled faster than
+# the next step comes back to the line) fetches every line twice (TCP->TCC
+# read requests r04l: DSD 1.3x, DDS 1.95x the algorithmic L2->L1 bytes). Its
+# ring becomes two double slots [128 rows][128 B] (16 KiB, chunk c of row r
+# at c ^ ((r >> 1) & 7): 16-B fragment reads stay bank-conflict free), filled
+# on odd steps for the next block-half; the other image keeps its 4 x 8 KiB
+# ring. LDS per wave and in total are unchanged.
+DS_SLOT = 16384
+
+
+def per_step_dmas(slot):
+    """(m0, load) pairs of the per-step image's DMAs into ring slot `slot`:
+    DSD the wave's D image (8 x 4 k-rows), DDS the shared S slice (2 x 4
+    k-rows of this wave's 8)."""
+    if VARIANT["dds"]:
+        return [(f"s_add_u32 m0, %[ms], {slot * SLOT + q * 1024}",
+                 f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} "
+                 f"offen lds") for q in range(2)]
+    return [(f"s_add_u32 m0, %[md], {slot * SLOT + q * 1024}",
+             f"buffer_load_dwordx4 %[vd{(q >> 1) & 1}], s[44:47], s{64 + q} offen lds")
+            for q in range(8)]
+
+
+def ds_dmas(d):
+    """(m0, load) pairs filling double slot d with 8-row x 128-B pieces: DSD
+    this wave's 32 rows of the shared S image (rows 32 w + 16 p + 8 q + l / 8:
+    %[vs<q>], soffset p x 16 rows), DDS the wave's 128 rows of A (rows 16 p +
+    8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows)."""
+    if VARIANT["dds"]:
+        return [(f"s_add_u32 m0, %[md], {d * DS_SLOT + q * 1024}",
+                 f"buffer_load_dwordx4 %[vd{q & 1}], s[44:47], s{64 + (q >> 1)} offen lds")
+                for q in range(16)]
+    return [(f"s_add_u32 m0, %[ms], {d * DS_SLOT + (2 * p + q) * 1024}",
+             f"buffer_load_dwordx4 {'%[vs]' if q == 0 else '%[vs1]'}, s[40:43], "
+             f"{'0' if p == 0 else 's72'} offen lds")
+            for p in range(2) for q in range(2)]
+
+
+def s_reads_ds(d, half, s):
+    """The 8 row-tile fragments (ds_read_b128) of step half `half` of double
+    slot d: chunk g + 4 half of the 128-B row, i.e. the half-0 lane address
+    with bit 6 flipped (%[vrs1] = %[vrs] ^ 64)."""
+    v = "%[vrs]" if half == 0 else "%[vrs1]"
+    return [f"ds_read_b128 v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], {v} "
+            f"offset:{d * DS_SLOT + m * 2048}" for m in range(8)]
+
+
+def advance_per_step():
+    return (["s_add_u32 s40, s40, 8192", "s_addc_u32 s41, s41, 0"] if VARIANT["dds"]
+            else ["s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"])
+
+
+def advance_ds():
+    return (["s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"] if VARIANT["dds"]
+            else ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0"])
+
+
+def ds_counts():
+    """DMA instructions a wave issues in an (odd, even) step."""
+    return (18, 2) if VARIANT["dds"] else (12, 8)
+
+
+def step_ds(dt, H, zero_c=False):
+    """Step H of a block in double-slot mode: as step(), with the per-step
+    image's DMAs of step + 3 every step and the double slot of steps + 3 and
+    + 4 on odd H (fed steps 0-1 / 2-3 of a block). At gap 1 every DMA of
+    step - 2 has landed (in-order vmcnt: step - 1's may fly), which covers
+    both images of step + 1. The shared double slot of DSD is refilled only
+    after this step's barrier: its previous steps were read up to the step
+    before (every wave has finished that step once all passed the barrier)."""
+    dds = VARIANT["dds"]
+    cur, nxt = H % 2, 1 - H % 2
+    gaps = [[] for _ in range(64)]
+    if H == 0:
+        gaps[0] += idx_load()
+    n_odd, n_even = ds_counts()
+    gaps[1].append(f"s_waitcnt vmcnt({n_odd if (H - 1) % 2 == 1 else n_even})")
+    if H == 1:
+        gaps[1] += switch()
+    s1 = (H + 1) % 4
+    tr = d_reads(s1, nxt)
+    kc = s_reads_ds(s1 // 2, s1 % 2, nxt)
+    own, shared = (kc, tr) if dds else (tr, kc)
+    for i, ins in enumerate(own):
+        gaps[READS_AT + i].append(ins)
+    bar = READS_AT + len(own)
+    gaps[bar].append("s_barrier")
+    for i, ins in enumerate(shared):
+        gaps[bar + 1 + i].append(ins)
+    fed = (H + 3) % 4
+    if dds:
+        pos_per, pos_ds = [3, 9], [13 + 3 * i for i in range(16)]
+    else:
+        pos_per, pos_ds = [3, 9, 15, 21, 27, 33, 39, 45], [30, 36, 42, 48]
+    placed = list(zip(per_step_dmas(fed), pos_per))
+    if H % 2 == 1:
+        placed += list(zip(ds_dmas(fed // 2), pos_ds))
+    for (m0, ld), k in placed:
+        gaps[k - 1].append(m0)
+        gaps[k].append(ld)
+    if H != 0:
+        gaps[59] += advance_per_step()
+    if H == 1:
+        gaps[59] += advance_ds()
+    gaps[63].append("s_waitcnt lgkmcnt(0)")
+    out = []
+    for i in range(64):
+        out.append(mfma(dt, i // 8, i % 8, cur, zero_c))
+        out += gaps[i]
+    return out
+
+
+def prologue_ds():
+    """Block 0: per-step slot 0, double slot 0 (steps 0-1), per-step slot 1;
+    wait for the first two; barrier; step 0's reads; per-step slot 2 and
+    double slot 1 (steps 2-3). The first loop step (H = 0) then waits with
+    the count of an odd step (slot 1 and double slot 0 landed)."""
+    out = prologue_setup()
+
+    def issue(pairs):
+        r = []
+        for m0, ld in pairs:
+            r += [m0, "s_nop 0", ld]
+        return r
+    out += issue(per_step_dmas(0)) + advance_per_step()
+    out += issue(ds_dmas(0)) + advance_ds()
+    out += issue(per_step_dmas(1)) + advance_per_step()
+    out += [f"s_waitcnt vmcnt({ds_counts()[1]})", "s_barrier"]
+    out += d_reads(0, 0) + s_reads_ds(0, 0, 0)
+    out += issue(per_step_dmas(2)) + advance_per_step()
+    out += issue(ds_dmas(1))
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
 def convert(cvt, i):
     """Accumulator i (m = i / 8, n = i % 8) -> fp16 / bf16 pairs -> the
     wave's staging region (per-wave layout, see epilogue_body)."""
@@ -222,6 +364,28 @@ def convert(cvt, i):
 
 
 def prologue():
+    if VARIANT["ds"]:
+        return prologue_ds()
+    out = prologue_setup()
+    # steps 0 and 1, wait for step 0 only, then step 2's DMA issued behind
+    # the step-0 fragment reads: the CU's TA serializes the 30 DMAs of every
+    # wave, and only step 0 is needed before the first MFMA
+    for slot in range(2):
+        for m0, ld in dmas(slot):
+            out += [m0, "s_nop 0", ld]
+        out += advance()
+    # (no accumulator zeroing: the first step's MFMAs take C = 0)
+    out += ["s_waitcnt vmcnt(10)", "s_barrier"]
+    out += d_reads(0, 0) + s_reads(0, 0)
+    for m0, ld in dmas(2):
+        out += [m0, "s_nop 0", ld]
+    out += advance()
+    out.append("s_waitcnt lgkmcnt(0)")
+    return out
+
+
+def prologue_setup():
+    """Descriptors, loop state, soffsets and block 0's S / D bases."""
     out = ["s_mov_b32 s42, 0x7fffffff", "s_mov_b32 s43, 0x00020000",
            "s_mov_b32 s46, 0x7fffffff", "s_mov_b32 s47, 0x00020000",
            "s_mov_b32 s84, %[pdlo]", "s_mov_b32 s85, %[pdhi]",
@@ -241,20 +405,6 @@ def prologue():
     out += ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
             "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
-    # steps 0 and 1, wait for step 0 only, then step 2's DMA issued behind
-    # the step-0 fragment reads: the CU's TA serializes the 30 DMAs of every
-    # wave, and only step 0 is needed before the first MFMA
-    for slot in range(2):
-        for m0, ld in dmas(slot):
-            out += [m0, "s_nop 0", ld]
-        out += advance()
-    # (no accumulator zeroing: the first step's MFMAs take C = 0)
-    out += ["s_waitcnt vmcnt(10)", "s_barrier"]
-    out += d_reads(0, 0) + s_reads(0, 0)
-    for m0, ld in dmas(2):
-        out += [m0, "s_nop 0", ld]
-    out += advance()
-    out.append("s_waitcnt lgkmcnt(0)")
     return out
 
 
@@ -381,12 +531,12 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False):
-    VARIANT["dds"] = dds
+def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False):
+    VARIANT["dds"], VARIANT["ds"] = dds, ds
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT["dds"] = False
+        VARIANT["dds"], VARIANT["ds"] = False, False
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -479,10 +629,13 @@ def render():
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_T \\")
         lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, True)]
         lines += ['  ""', ""]
-        # DDS NN (dds4w, the same kernel with the operand images swapped)
-        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_DDS \\")
-        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, True)]
-        lines += ['  ""', ""]
+        # DDS NN (the same kernel with the operand images swapped); _W2: the
+        # double-slot k-contiguous image, DSD and DDS
+        for name, dds, ds in (("_W_DDS", True, False), ("_W2", False, True),
+                              ("_W2_DDS", True, True)):
+            lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
+            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, dds, ds)]
+            lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]
             + [f'"s{i}"' for i in range(84, 88)] + [f'"s{i}"' for i in range(96, 100)]

@@ -49,8 +49,8 @@ def _problem(m, k, n, density, dtype, seed, empty_rows=()):
 
 def _run(A, B, m, n, dtype, mode):
     """mode: 0 the 8-wave kernel, 2 the 4-wave kernel (workgroup epilogue),
-    3 with the per-wave epilogue, 4 per-wave + specialized last block; 2-4
-    regardless of the density gate."""
+    3 with the per-wave epilogue, 4 per-wave + specialized last block, 5
+    per-wave + double-slot S image; 2-5 regardless of the density gate."""
     td = torch.float16 if dtype == "f16" else torch.bfloat16
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
     prev = sp.select_dsd_kernel(mode)
@@ -78,7 +78,7 @@ CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("mode", [2, 3, 4])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5])
 def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
     c4 = _run(A, B, m, n, dtype, mode)
@@ -89,7 +89,7 @@ def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     assert sp.pair_errors() == 0
 
 
-@pytest.mark.parametrize("mode", [2, 3, 4])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5])
 def test_dsd4w_empty_rows_and_oracle(mode):
     """Empty block-rows get zero tiles; sampled rows against the oracle."""
     m, k, n = 4096, 2048, 1024
@@ -114,7 +114,7 @@ def test_dsd4w_empty_rows_and_oracle(mode):
 
 def test_dsd4w_selector_roundtrip():
     prev = sp.select_dsd_kernel(-1)
-    assert prev in (0, 1, 2, 3, 4)
+    assert prev in (0, 1, 2, 3, 4, 5)
     assert sp.select_dsd_kernel(0) == prev
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0
@@ -179,10 +179,12 @@ DDS_CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", DDS_CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_dds4w_bit_identical_to_8wave(m, k, n, density, dtype):
+@pytest.mark.parametrize("mode", [3, 5])
+def test_dds4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
+    """mode 3: per-step rows of A; 5: double slots of 128-B row pieces."""
     A, B, off, idx, a, b = _dds_problem(m, k, n, density, dtype,
                                         seed=m + 3 * n + int(density * 100))
-    c4 = _run_dds(A, B, m, n, dtype, 3)
+    c4 = _run_dds(A, B, m, n, dtype, mode)
     c8 = _run_dds(A, B, m, n, dtype, 0)
     assert not torch.isnan(c4.float()).any()
     assert torch.equal(c4, c8), (
@@ -190,11 +192,12 @@ def test_dds4w_bit_identical_to_8wave(m, k, n, density, dtype):
     assert sp.pair_errors() == 0
 
 
-def test_dds4w_empty_columns_and_oracle():
+@pytest.mark.parametrize("mode", [3, 5])
+def test_dds4w_empty_columns_and_oracle(mode):
     m, k, n = 1536, 2048, 4096
     A, B, off, idx, a, b = _dds_problem(m, k, n, 0.5, "f16", seed=5,
                                         empty_cols=(0, 7, 31))
-    c4 = _run_dds(A, B, m, n, "f16", 3)
+    c4 = _run_dds(A, B, m, n, "f16", mode)
     c8 = _run_dds(A, B, m, n, "f16", 0)
     assert torch.equal(c4, c8)
     for c in (0, 7, 31):
