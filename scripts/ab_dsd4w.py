@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--calls", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--dim", type=int, default=4096)
-    ap.add_argument("--op", default="dsd", choices=["dsd", "dds"],
-                    help="dds: bench.py's OpProblem DDS NN (the kDds kernel)")
+    ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"],
+                    help="dds / sdd: bench.py's OpProblem DDS NN / SDD NN")
+    ap.add_argument("--calls-scale", type=float, default=1.0)
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,8 +37,8 @@ def main():
         rng = np.random.default_rng(1)
         nz = mu.nonzeros_for_density(d, d, dens)
         off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
-        if a.op == "dds":
-            ns = argparse.Namespace(op="dds", trans="NN", api="ex", k=d,
+        if a.op in ("dds", "sdd"):
+            ns = argparse.Namespace(op=a.op, trans="NN", api="ex", k=d,
                                     density=dens, dtype=a.dtype, seed=0)
             prob = bench.OpProblem(ns, dev)
         else:
@@ -55,7 +56,8 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(e) * 1e3 / a.calls
 
-        arms = {"8wave": 0, "4wave": 3, "4wave_ds": 5}
+        arms = ({"8wave": 0, "4wave": 1} if a.op == "sdd"
+                else {"8wave": 0, "4wave": 3, "4wave_ds": 5})
         for mode in arms.values():
             timed(mode)
             for _ in range(100):

@@ -108,7 +108,15 @@ def dmas(slot):
 # DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
-VARIANT = {"dds": False, "ds": False}
+VARIANT = {"dds": False, "ds": False, "sdd": False}
+# SDD (grouped, NN): the shared image is the row panel of A, so entry x (=
+# k-block x: no index list) starts 256 B into its rows, not at a stored
+# block; the 16-row soffset is 16 lda (%[s16]).
+
+
+def s_block_shift():
+    """(high, low) shifts of S's byte offset from the entry in s76."""
+    return (24, 8) if VARIANT["sdd"] else (17, 15)
 
 
 def advance():
@@ -134,9 +142,10 @@ def switch():
     if VARIANT["dds"]:
         blk = ["s_lshr_b32 s77, s63, 17", "s_lshl_b32 s76, s63, 15"]
     else:
+        hi, lo = s_block_shift()
         blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
                + entry_of("s57", "s76")
-               + ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15"])
+               + [f"s_lshr_b32 s77, s76, {hi}", f"s_lshl_b32 s76, s76, {lo}"])
     out = blk + ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
                  "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
                  "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
@@ -148,6 +157,8 @@ def switch():
 # Scalar load of the k-block (int16) of virtual entry min(s56, xlast) into
 # s59 (its half in s60), one block ahead of the SWITCH that uses it.
 def idx_load():
+    if VARIANT["sdd"]:  # k-block of virtual entry x is x
+        return ["s_min_u32 s59, s56, %[xlast]", "s_add_u32 s56, s56, 1", "s_mov_b32 s60, 0"]
     out = ["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"] + entry_of("s78", "s79")
     if VARIANT["dds"]:
         out += ["s_lshl_b32 s74, s79, 2", "s_add_u32 s74, %[bolo], s74",
@@ -392,7 +403,9 @@ def prologue_setup():
            "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
            "s_mov_b32 s56, 2", "s_mov_b32 s57, 0",
            "s_mov_b32 s58, %[kb1]", "s_mov_b32 s61, %[ntot]",
-           f"s_mov_b32 s72, {1024 if VARIANT['dds'] else 4096}", "s_mov_b32 s64, 0"]
+           "s_mov_b32 s72, " + ("%[s16]" if VARIANT["sdd"] else
+                                f"{1024 if VARIANT['dds'] else 4096}"),
+           "s_mov_b32 s64, 0"]
     out += [f"s_mul_i32 s{64 + q}, %[k4], {q}" for q in range(1, 8)]
     # block 0: virtual entry 0, k-block kb0 (DDS: storage block bo0; s63 =
     # entry 1's, bo1)
@@ -400,8 +413,9 @@ def prologue_setup():
         out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
                 "s_mov_b32 s63, %[bo1]"]
     else:
+        hi, lo = s_block_shift()
         out += entry_of("s57", "s76")
-        out += ["s_lshr_b32 s77, s76, 17", "s_lshl_b32 s76, s76, 15"]
+        out += [f"s_lshr_b32 s77, s76, {hi}", f"s_lshl_b32 s76, s76, {lo}"]
     out += ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
             "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
@@ -531,12 +545,13 @@ def poll():
             "s_branch L_nan_%="]
 
 
-def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False):
-    VARIANT["dds"], VARIANT["ds"] = dds, ds
+def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
+          sdd=False):
+    VARIANT["dds"], VARIANT["ds"], VARIANT["sdd"] = dds, ds, sdd
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT["dds"], VARIANT["ds"] = False, False
+        VARIANT["dds"], VARIANT["ds"], VARIANT["sdd"] = False, False, False
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -631,10 +646,10 @@ def render():
         lines += ['  ""', ""]
         # DDS NN (the same kernel with the operand images swapped); _W2: the
         # double-slot k-contiguous image, DSD and DDS
-        for name, dds, ds in (("_W_DDS", True, False), ("_W2", False, True),
-                              ("_W2_DDS", True, True)):
+        for name, dds, ds, sdd in (("_W_DDS", True, False, False), ("_W2", False, True, False),
+                                   ("_W2_DDS", True, True, False), ("_W2_SDD", False, True, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
-            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, dds, ds)]
+            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, dds, ds, sdd)]
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

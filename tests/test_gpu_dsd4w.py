@@ -213,3 +213,79 @@ def test_dds4w_empty_columns_and_oracle(mode):
         ref = O.gemm(av, False, col, False, threads=H.oracle_threads())
         H.assert_close(c4[:, c * 128:(c + 1) * 128].float().cpu().numpy(), ref,
                        "f16", f"dds4w block-column {c}")
+
+
+# ------------------------------------------------------------ grouped SDD --
+# The same kernel on the grouped SDD NN launch (dsd4w.hip kSdd: up to 4
+# stored blocks of a block-row per workgroup): against the 8-wave grouped
+# kernel (same k order and MFMA operand roles: torch.equal) and the oracle.
+
+def _sdd_problem(m, k, n, density, dtype, seed, uniform=0):
+    rng = np.random.default_rng(seed)
+    R, C = m // 128, n // 128
+    if uniform:
+        off = np.arange(R + 1, dtype=np.int32) * uniform
+        idx = np.concatenate([np.sort(rng.choice(C, uniform, replace=False))
+                              for _ in range(R)]).astype(np.int16)
+    else:
+        nz = mu.nonzeros_for_density(m, n, density) // (128 * 128)
+        off, idx = mu.random_topology(R, C, nz, rng)
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    a = (torch.rand(m * k, generator=g, device="cuda") * 2 - 1).to(td)
+    b = (torch.rand(k * n, generator=g, device="cuda") * 2 - 1).to(td)
+    nb = int(off[-1])
+    cv = torch.full((nb * 16384,), float("nan"), dtype=td, device="cuda")
+    Cm = sp.BlockMatrix(m, n, 128, nb * 16384, cv,
+                        torch.from_numpy(np.asarray(off, np.int32)).cuda(),
+                        torch.from_numpy(np.asarray(idx).astype(np.int16)).cuda())
+    sp.AllocateRowIndicesBuffer(Cm)
+    sp.RowIndices(Cm, Cm.row_indices)
+    return sp.Matrix(m, k, a), sp.Matrix(k, n, b), Cm, cv, off, idx, a, b
+
+
+def _run_sdd(A, B, Cm, cv, mode):
+    cv.fill_(float("nan"))
+    prev = sp.select_dsd_kernel(mode)
+    try:
+        sp.Matmul(A, False, B, False, Cm)
+        torch.cuda.synchronize()
+    finally:
+        sp.select_dsd_kernel(prev)
+    return cv.clone()
+
+
+SDD_CASES = [
+    # m, k, n, density, uniform blocks per row (0: random)
+    (8192, 1024, 8192, 0.5, 0),     # 2048 blocks: grouped
+    (8192, 2048, 8192, 0.4, 0),
+    (8192, 512, 16384, 0.2, 0),
+    (8192, 1024, 8192, 0, 27),      # uniform rows: group-major order, partial groups
+]
+
+
+@pytest.mark.parametrize("m,k,n,density,uniform", SDD_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype):
+    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, density, dtype,
+                                                seed=m + k + n, uniform=uniform)
+    c4 = _run_sdd(A, B, Cm, cv, 1)
+    c8 = _run_sdd(A, B, Cm, cv, 0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+
+
+def test_sdd4w_oracle():
+    m, k, n = 8192, 1024, 8192
+    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, 0.5, "f16", seed=11)
+    c4 = _run_sdd(A, B, Cm, cv, 1).view(-1, 128, 128).float().cpu().numpy()
+    av = a.float().cpu().numpy().reshape(m, k)
+    bv = b.float().cpu().numpy().reshape(k, n)
+    rows = np.repeat(np.arange(m // 128), np.diff(off))
+    for e in (0, 1, 2, 3, 5, 777, int(off[-1]) - 1):
+        r, c = int(rows[e]), int(idx[e])
+        ref = O.gemm(av[r * 128:(r + 1) * 128], False, bv[:, c * 128:(c + 1) * 128],
+                     False, threads=H.oracle_threads())
+        H.assert_close(c4[e], ref, "f16", f"sdd4w block {e}")
