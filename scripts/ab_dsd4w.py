@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--dim", type=int, default=4096)
     ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"],
                     help="dds / sdd: bench.py's OpProblem DDS NN / SDD NN")
-    ap.add_argument("--calls-scale", type=float, default=1.0)
+    ap.add_argument("--trans", default="NN")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -38,7 +38,7 @@ def main():
         nz = mu.nonzeros_for_density(d, d, dens)
         off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
         if a.op in ("dds", "sdd"):
-            ns = argparse.Namespace(op=a.op, trans="NN", api="ex", k=d,
+            ns = argparse.Namespace(op=a.op, trans=a.trans, api="ex", k=d,
                                     density=dens, dtype=a.dtype, seed=0)
             prob = bench.OpProblem(ns, dev)
         else:
@@ -69,7 +69,7 @@ def main():
                 ts[k].append(timed(mode))
         sp.select_dsd_kernel(1)
         med = lambda v: sorted(v)[len(v) // 2]
-        out = {"op": a.op, "density": dens, "dtype": a.dtype, "dim": d}
+        out = {"op": a.op, "trans": a.trans, "density": dens, "dtype": a.dtype, "dim": d}
         for k, v in ts.items():
             out[k] = {"us": round(med(v), 2),
                       "tflops": round(prob.flops / med(v) / 1e6, 1),

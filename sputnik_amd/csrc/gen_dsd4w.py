@@ -108,7 +108,12 @@ def dmas(slot):
 # DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
-VARIANT = {"dds": False, "ds": False, "sdd": False}
+VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False}
+# SDD NT ("nt", with "sdd" and "ds"): B stored [n][k], so the wave's image is
+# k-contiguous too: both images in double slots, both read with ds_read_b128
+# (the wave's B rows into the MFMA's A-operand set, %[vrd0] / %[vrd1] =
+# half-0 / half-1 addresses), and every DMA is a double-slot one, on odd
+# steps.
 # SDD (grouped, NN): the shared image is the row panel of A, so entry x (=
 # k-block x: no index list) starts 256 B into its rows, not at a stored
 # block; the 16-row soffset is 16 lda (%[s16]).
@@ -241,7 +246,9 @@ DS_SLOT = 16384
 def per_step_dmas(slot):
     """(m0, load) pairs of the per-step image's DMAs into ring slot `slot`:
     DSD the wave's D image (8 x 4 k-rows), DDS the shared S slice (2 x 4
-    k-rows of this wave's 8)."""
+    k-rows of this wave's 8); SDD NT none."""
+    if VARIANT["nt"]:
+        return []
     if VARIANT["dds"]:
         return [(f"s_add_u32 m0, %[ms], {slot * SLOT + q * 1024}",
                  f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} "
@@ -251,15 +258,20 @@ def per_step_dmas(slot):
             for q in range(8)]
 
 
+def own_ds_dmas(d):
+    return [(f"s_add_u32 m0, %[md], {d * DS_SLOT + q * 1024}",
+             f"buffer_load_dwordx4 %[vd{q & 1}], s[44:47], s{64 + (q >> 1)} offen lds")
+            for q in range(16)]
+
+
 def ds_dmas(d):
     """(m0, load) pairs filling double slot d with 8-row x 128-B pieces: DSD
     this wave's 32 rows of the shared S image (rows 32 w + 16 p + 8 q + l / 8:
     %[vs<q>], soffset p x 16 rows), DDS the wave's 128 rows of A (rows 16 p +
-    8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows)."""
+    8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows). (SDD NT: the
+    shared one here, the wave's own in own_ds_dmas.)"""
     if VARIANT["dds"]:
-        return [(f"s_add_u32 m0, %[md], {d * DS_SLOT + q * 1024}",
-                 f"buffer_load_dwordx4 %[vd{q & 1}], s[44:47], s{64 + (q >> 1)} offen lds")
-                for q in range(16)]
+        return own_ds_dmas(d)
     return [(f"s_add_u32 m0, %[ms], {d * DS_SLOT + (2 * p + q) * 1024}",
              f"buffer_load_dwordx4 {'%[vs]' if q == 0 else '%[vs1]'}, s[40:43], "
              f"{'0' if p == 0 else 's72'} offen lds")
@@ -276,18 +288,33 @@ def s_reads_ds(d, half, s):
 
 
 def advance_per_step():
+    if VARIANT["nt"]:
+        return []
     return (["s_add_u32 s40, s40, 8192", "s_addc_u32 s41, s41, 0"] if VARIANT["dds"]
             else ["s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"])
 
 
 def advance_ds():
+    if VARIANT["nt"]:
+        return ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0",
+                "s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"]
     return (["s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"] if VARIANT["dds"]
             else ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0"])
 
 
 def ds_counts():
     """DMA instructions a wave issues in an (odd, even) step."""
+    if VARIANT["nt"]:
+        return (20, 0)
     return (18, 2) if VARIANT["dds"] else (12, 8)
+
+
+def own_reads_kc(d, half, s):
+    """SDD NT: the wave's 8 column-tile fragments (ds_read_b128 of its B
+    rows) into the A-operand set."""
+    v = "%[vrd0]" if half == 0 else "%[vrd1]"
+    return [f"ds_read_b128 v[{FD[s] + 4 * n}:{FD[s] + 4 * n + 3}], {v} "
+            f"offset:{d * DS_SLOT + n * 2048}" for n in range(8)]
 
 
 def step_ds(dt, H, zero_c=False):
@@ -308,9 +335,12 @@ def step_ds(dt, H, zero_c=False):
     if H == 1:
         gaps[1] += switch()
     s1 = (H + 1) % 4
-    tr = d_reads(s1, nxt)
     kc = s_reads_ds(s1 // 2, s1 % 2, nxt)
-    own, shared = (kc, tr) if dds else (tr, kc)
+    if VARIANT["nt"]:
+        own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), kc
+    else:
+        tr = d_reads(s1, nxt)
+        own, shared = (kc, tr) if dds else (tr, kc)
     for i, ins in enumerate(own):
         gaps[READS_AT + i].append(ins)
     bar = READS_AT + len(own)
@@ -318,20 +348,27 @@ def step_ds(dt, H, zero_c=False):
     for i, ins in enumerate(shared):
         gaps[bar + 1 + i].append(ins)
     fed = (H + 3) % 4
-    if dds:
+    if VARIANT["nt"]:
+        # the wave's own double slot anywhere, the shared one after the
+        # barrier (gap 10)
+        pos_per, pos_ds = [], [51, 54, 57, 60]
+    elif dds:
         pos_per, pos_ds = [3, 9], [13 + 3 * i for i in range(16)]
     else:
         pos_per, pos_ds = [3, 9, 15, 21, 27, 33, 39, 45], [30, 36, 42, 48]
     placed = list(zip(per_step_dmas(fed), pos_per))
     if H % 2 == 1:
         placed += list(zip(ds_dmas(fed // 2), pos_ds))
+        if VARIANT["nt"]:
+            placed += list(zip(own_ds_dmas(fed // 2), [3 + 3 * i for i in range(16)]))
     for (m0, ld), k in placed:
         gaps[k - 1].append(m0)
         gaps[k].append(ld)
+    adv = 61 if VARIANT["nt"] else 59   # after the step's last DMA
     if H != 0:
-        gaps[59] += advance_per_step()
+        gaps[adv] += advance_per_step()
     if H == 1:
-        gaps[59] += advance_ds()
+        gaps[adv] += advance_ds()
     gaps[63].append("s_waitcnt lgkmcnt(0)")
     out = []
     for i in range(64):
@@ -352,13 +389,14 @@ def prologue_ds():
         for m0, ld in pairs:
             r += [m0, "s_nop 0", ld]
         return r
+    own_ds = own_ds_dmas if VARIANT["nt"] else (lambda d: [])
     out += issue(per_step_dmas(0)) + advance_per_step()
-    out += issue(ds_dmas(0)) + advance_ds()
+    out += issue(ds_dmas(0)) + issue(own_ds(0)) + advance_ds()
     out += issue(per_step_dmas(1)) + advance_per_step()
     out += [f"s_waitcnt vmcnt({ds_counts()[1]})", "s_barrier"]
-    out += d_reads(0, 0) + s_reads_ds(0, 0, 0)
+    out += (own_reads_kc(0, 0, 0) if VARIANT["nt"] else d_reads(0, 0)) + s_reads_ds(0, 0, 0)
     out += issue(per_step_dmas(2)) + advance_per_step()
-    out += issue(ds_dmas(1))
+    out += issue(ds_dmas(1)) + issue(own_ds(1))
     out.append("s_waitcnt lgkmcnt(0)")
     return out
 
@@ -546,12 +584,12 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False):
-    VARIANT["dds"], VARIANT["ds"], VARIANT["sdd"] = dds, ds, sdd
+          sdd=False, nt=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT["dds"], VARIANT["ds"], VARIANT["sdd"] = False, False, False
+        VARIANT.update(dds=False, ds=False, sdd=False, nt=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -646,10 +684,14 @@ def render():
         lines += ['  ""', ""]
         # DDS NN (the same kernel with the operand images swapped); _W2: the
         # double-slot k-contiguous image, DSD and DDS
-        for name, dds, ds, sdd in (("_W_DDS", True, False, False), ("_W2", False, True, False),
-                                   ("_W2_DDS", True, True, False), ("_W2_SDD", False, True, True)):
+        for name, dds, ds, sdd, nt in (("_W_DDS", True, False, False, False),
+                                       ("_W2", False, True, False, False),
+                                       ("_W2_DDS", True, True, False, False),
+                                       ("_W2_SDD", False, True, True, False),
+                                       ("_W2_SDD_NT", False, True, True, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
-            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, False, False, dds, ds, sdd)]
+            lines += [f'  "{ins}\\n" \\'
+                      for ins in build(dt, True, False, False, dds, ds, sdd, nt)]
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

@@ -220,7 +220,7 @@ def test_dds4w_empty_columns_and_oracle(mode):
 # stored blocks of a block-row per workgroup): against the 8-wave grouped
 # kernel (same k order and MFMA operand roles: torch.equal) and the oracle.
 
-def _sdd_problem(m, k, n, density, dtype, seed, uniform=0):
+def _sdd_problem(m, k, n, density, dtype, seed, uniform=0, tb=False):
     rng = np.random.default_rng(seed)
     R, C = m // 128, n // 128
     if uniform:
@@ -242,14 +242,15 @@ def _sdd_problem(m, k, n, density, dtype, seed, uniform=0):
                         torch.from_numpy(np.asarray(idx).astype(np.int16)).cuda())
     sp.AllocateRowIndicesBuffer(Cm)
     sp.RowIndices(Cm, Cm.row_indices)
-    return sp.Matrix(m, k, a), sp.Matrix(k, n, b), Cm, cv, off, idx, a, b
+    Bm = sp.Matrix(n, k, b) if tb else sp.Matrix(k, n, b)
+    return sp.Matrix(m, k, a), Bm, Cm, cv, off, idx, a, b
 
 
-def _run_sdd(A, B, Cm, cv, mode):
+def _run_sdd(A, B, Cm, cv, mode, tb=False):
     cv.fill_(float("nan"))
     prev = sp.select_dsd_kernel(mode)
     try:
-        sp.Matmul(A, False, B, False, Cm)
+        sp.Matmul(A, False, B, tb, Cm)
         torch.cuda.synchronize()
     finally:
         sp.select_dsd_kernel(prev)
@@ -267,22 +268,25 @@ SDD_CASES = [
 
 @pytest.mark.parametrize("m,k,n,density,uniform", SDD_CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype):
+@pytest.mark.parametrize("tb", [False, True])
+def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, tb):
     A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, density, dtype,
-                                                seed=m + k + n, uniform=uniform)
-    c4 = _run_sdd(A, B, Cm, cv, 1)
-    c8 = _run_sdd(A, B, Cm, cv, 0)
+                                                seed=m + k + n, uniform=uniform, tb=tb)
+    c4 = _run_sdd(A, B, Cm, cv, 1, tb)
+    c8 = _run_sdd(A, B, Cm, cv, 0, tb)
     assert not torch.isnan(c4.float()).any()
     assert torch.equal(c4, c8), (
         f"max diff {float((c4.float() - c8.float()).abs().max())}")
 
 
-def test_sdd4w_oracle():
+@pytest.mark.parametrize("tb", [False, True])
+def test_sdd4w_oracle(tb):
     m, k, n = 8192, 1024, 8192
-    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, 0.5, "f16", seed=11)
-    c4 = _run_sdd(A, B, Cm, cv, 1).view(-1, 128, 128).float().cpu().numpy()
+    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, 0.5, "f16", seed=11, tb=tb)
+    c4 = _run_sdd(A, B, Cm, cv, 1, tb).view(-1, 128, 128).float().cpu().numpy()
     av = a.float().cpu().numpy().reshape(m, k)
-    bv = b.float().cpu().numpy().reshape(k, n)
+    bv = b.float().cpu().numpy().reshape(n, k).T if tb else \
+        b.float().cpu().numpy().reshape(k, n)
     rows = np.repeat(np.arange(m // 128), np.diff(off))
     for e in (0, 1, 2, 3, 5, 777, int(off[-1]) - 1):
         r, c = int(rows[e]), int(idx[e])
