@@ -937,7 +937,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   p.debug = g_debug;
   const bool grouped = UseGroupedSdd(&p, c, tb);
   if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb))
-    return LaunchSdd4w(dtype, p, tb, stream);
+    return LaunchSdd4w(dtype, p, ta, tb, stream);
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
                          grouped, p, stream);
 }

@@ -44,11 +44,12 @@ bool Dds4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
                   bool out_t, bool tall);
 hipError_t LaunchDds4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
 
-// Grouped SDD NN / NT (dispatch.cpp UseGroupedSdd: up to 4 stored blocks
-// of a block-row per workgroup, grid = the group count's upper bound), K a
-// multiple of 128: dsd4w.hip kSdd / kNt.
+// Grouped SDD NN / NT / TT (dispatch.cpp UseGroupedSdd: up to 4 stored
+// blocks of a block-row per workgroup, grid = the group count's upper
+// bound), K a multiple of 128: dsd4w.hip kSdd / kNt / kTt.
 bool Sdd4wApplies(const GemmParams &p, bool grouped, bool ta, bool tb);
-hipError_t LaunchSdd4w(int dtype, const GemmParams &p, bool tb, hipStream_t stream);
+hipError_t LaunchSdd4w(int dtype, const GemmParams &p, bool ta, bool tb,
+                       hipStream_t stream);
 
 }  // namespace sputnik_amd
 

@@ -72,10 +72,12 @@ def mfma(dt, m, n, s, zero_c=False):
             f"v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], {c}")
 
 
-def d_reads(slot, s):
+def d_reads(slot, s, into=None):
+    """The 8 transposed fragments of a [32 k][128] image in ring slot
+    `slot` (by default into the A-operand set; SDD TT: the B-operand set)."""
     out = []
     for n in range(8):
-        b = FD[s] + 4 * n
+        b = (into or FD)[s] + 4 * n
         out.append(f"ds_read_b64_tr_b16 v[{b}:{b + 1}], %[vrd{n}] offset:{slot * SLOT}")
         out.append(f"ds_read_b64_tr_b16 v[{b + 2}:{b + 3}], %[vrd{n}] "
                    f"offset:{slot * SLOT + 1024}")
@@ -108,10 +110,16 @@ def dmas(slot):
 # DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
-VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False}
+VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False}
+# SDD TT ("tt", with "sdd" and "ds"): A stored [k][m], so the shared image is
+# the per-step [32 k][128 m] slice of A (rows lda apart: %[s16] = 4 lda
+# between its two DMAs, S advances %[sk32] = 32 lda per step and %[sk128] per
+# k-block), read transposed into the MFMA's B-operand set; B stored [n][k]:
+# the wave's image in double slots as in NT. The DDS ring structure with the
+# operand sets exchanged.
 # SDD NT ("nt", with "sdd" and "ds"): B stored [n][k], so the wave's image is
 # k-contiguous too: both images in double slots, both read with ds_read_b128
-# (the wave's B rows into the MFMA's A-operand set, %[vrd0] / %[vrd1] =
+# (the wave's B rows into the MFMA's A-operand set, %[vrk0] / %[vrk1] =
 # half-0 / half-1 addresses), and every DMA is a double-slot one, on odd
 # steps.
 # SDD (grouped, NN): the shared image is the row panel of A, so entry x (=
@@ -146,6 +154,10 @@ def entry_of(xreg, out_reg):
 def switch():
     if VARIANT["dds"]:
         blk = ["s_lshr_b32 s77, s63, 17", "s_lshl_b32 s76, s63, 15"]
+    elif VARIANT["tt"]:
+        blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
+               + entry_of("s57", "s78")
+               + ["s_mul_hi_u32 s77, s78, %[sk128]", "s_mul_i32 s76, s78, %[sk128]"])
     else:
         hi, lo = s_block_shift()
         blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
@@ -245,11 +257,11 @@ DS_SLOT = 16384
 
 def per_step_dmas(slot):
     """(m0, load) pairs of the per-step image's DMAs into ring slot `slot`:
-    DSD the wave's D image (8 x 4 k-rows), DDS the shared S slice (2 x 4
-    k-rows of this wave's 8); SDD NT none."""
+    DSD the wave's D image (8 x 4 k-rows), DDS / SDD TT the shared S slice
+    (2 x 4 k-rows of this wave's 8); SDD NT none."""
     if VARIANT["nt"]:
         return []
-    if VARIANT["dds"]:
+    if VARIANT["dds"] or VARIANT["tt"]:
         return [(f"s_add_u32 m0, %[ms], {slot * SLOT + q * 1024}",
                  f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} "
                  f"offen lds") for q in range(2)]
@@ -270,7 +282,7 @@ def ds_dmas(d):
     %[vs<q>], soffset p x 16 rows), DDS the wave's 128 rows of A (rows 16 p +
     8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows). (SDD NT: the
     shared one here, the wave's own in own_ds_dmas.)"""
-    if VARIANT["dds"]:
+    if VARIANT["dds"] or VARIANT["tt"]:
         return own_ds_dmas(d)
     return [(f"s_add_u32 m0, %[ms], {d * DS_SLOT + (2 * p + q) * 1024}",
              f"buffer_load_dwordx4 {'%[vs]' if q == 0 else '%[vs1]'}, s[40:43], "
@@ -290,6 +302,8 @@ def s_reads_ds(d, half, s):
 def advance_per_step():
     if VARIANT["nt"]:
         return []
+    if VARIANT["tt"]:
+        return ["s_add_u32 s40, s40, %[sk32]", "s_addc_u32 s41, s41, 0"]
     return (["s_add_u32 s40, s40, 8192", "s_addc_u32 s41, s41, 0"] if VARIANT["dds"]
             else ["s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"])
 
@@ -298,7 +312,8 @@ def advance_ds():
     if VARIANT["nt"]:
         return ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0",
                 "s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"]
-    return (["s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"] if VARIANT["dds"]
+    return (["s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"]
+            if VARIANT["dds"] or VARIANT["tt"]
             else ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0"])
 
 
@@ -306,13 +321,13 @@ def ds_counts():
     """DMA instructions a wave issues in an (odd, even) step."""
     if VARIANT["nt"]:
         return (20, 0)
-    return (18, 2) if VARIANT["dds"] else (12, 8)
+    return (18, 2) if VARIANT["dds"] or VARIANT["tt"] else (12, 8)
 
 
 def own_reads_kc(d, half, s):
     """SDD NT: the wave's 8 column-tile fragments (ds_read_b128 of its B
     rows) into the A-operand set."""
-    v = "%[vrd0]" if half == 0 else "%[vrd1]"
+    v = "%[vrk0]" if half == 0 else "%[vrk1]"
     return [f"ds_read_b128 v[{FD[s] + 4 * n}:{FD[s] + 4 * n + 3}], {v} "
             f"offset:{d * DS_SLOT + n * 2048}" for n in range(8)]
 
@@ -338,6 +353,8 @@ def step_ds(dt, H, zero_c=False):
     kc = s_reads_ds(s1 // 2, s1 % 2, nxt)
     if VARIANT["nt"]:
         own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), kc
+    elif VARIANT["tt"]:
+        own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), d_reads(s1, nxt, FS)
     else:
         tr = d_reads(s1, nxt)
         own, shared = (kc, tr) if dds else (tr, kc)
@@ -352,7 +369,7 @@ def step_ds(dt, H, zero_c=False):
         # the wave's own double slot anywhere, the shared one after the
         # barrier (gap 10)
         pos_per, pos_ds = [], [51, 54, 57, 60]
-    elif dds:
+    elif dds or VARIANT["tt"]:
         pos_per, pos_ds = [3, 9], [13 + 3 * i for i in range(16)]
     else:
         pos_per, pos_ds = [3, 9, 15, 21, 27, 33, 39, 45], [30, 36, 42, 48]
@@ -394,7 +411,12 @@ def prologue_ds():
     out += issue(ds_dmas(0)) + issue(own_ds(0)) + advance_ds()
     out += issue(per_step_dmas(1)) + advance_per_step()
     out += [f"s_waitcnt vmcnt({ds_counts()[1]})", "s_barrier"]
-    out += (own_reads_kc(0, 0, 0) if VARIANT["nt"] else d_reads(0, 0)) + s_reads_ds(0, 0, 0)
+    if VARIANT["nt"]:
+        out += own_reads_kc(0, 0, 0) + s_reads_ds(0, 0, 0)
+    elif VARIANT["tt"]:
+        out += own_reads_kc(0, 0, 0) + d_reads(0, 0, FS)
+    else:
+        out += d_reads(0, 0) + s_reads_ds(0, 0, 0)
     out += issue(per_step_dmas(2)) + advance_per_step()
     out += issue(ds_dmas(1)) + issue(own_ds(1))
     out.append("s_waitcnt lgkmcnt(0)")
@@ -450,6 +472,8 @@ def prologue_setup():
     if VARIANT["dds"]:
         out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
                 "s_mov_b32 s63, %[bo1]"]
+    elif VARIANT["tt"]:  # entry 0: the panel's first k-block
+        out += ["s_mov_b32 s76, 0", "s_mov_b32 s77, 0"]
     else:
         hi, lo = s_block_shift()
         out += entry_of("s57", "s76")
@@ -584,12 +608,12 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False):
-    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt)
+          sdd=False, nt=False, tt=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT.update(dds=False, ds=False, sdd=False, nt=False)
+        VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -684,14 +708,15 @@ def render():
         lines += ['  ""', ""]
         # DDS NN (the same kernel with the operand images swapped); _W2: the
         # double-slot k-contiguous image, DSD and DDS
-        for name, dds, ds, sdd, nt in (("_W_DDS", True, False, False, False),
-                                       ("_W2", False, True, False, False),
-                                       ("_W2_DDS", True, True, False, False),
-                                       ("_W2_SDD", False, True, True, False),
-                                       ("_W2_SDD_NT", False, True, True, True)):
+        for name, dds, ds, sdd, nt, tt in (("_W_DDS", True, False, False, False, False),
+                                           ("_W2", False, True, False, False, False),
+                                           ("_W2_DDS", True, True, False, False, False),
+                                           ("_W2_SDD", False, True, True, False, False),
+                                           ("_W2_SDD_NT", False, True, True, True, False),
+                                           ("_W2_SDD_TT", False, True, True, False, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
-                      for ins in build(dt, True, False, False, dds, ds, sdd, nt)]
+                      for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

@@ -220,7 +220,7 @@ def test_dds4w_empty_columns_and_oracle(mode):
 # stored blocks of a block-row per workgroup): against the 8-wave grouped
 # kernel (same k order and MFMA operand roles: torch.equal) and the oracle.
 
-def _sdd_problem(m, k, n, density, dtype, seed, uniform=0, tb=False):
+def _sdd_problem(m, k, n, density, dtype, seed, uniform=0, tb=False, ta=False):
     rng = np.random.default_rng(seed)
     R, C = m // 128, n // 128
     if uniform:
@@ -243,14 +243,15 @@ def _sdd_problem(m, k, n, density, dtype, seed, uniform=0, tb=False):
     sp.AllocateRowIndicesBuffer(Cm)
     sp.RowIndices(Cm, Cm.row_indices)
     Bm = sp.Matrix(n, k, b) if tb else sp.Matrix(k, n, b)
-    return sp.Matrix(m, k, a), Bm, Cm, cv, off, idx, a, b
+    Am = sp.Matrix(k, m, a) if ta else sp.Matrix(m, k, a)
+    return Am, Bm, Cm, cv, off, idx, a, b
 
 
-def _run_sdd(A, B, Cm, cv, mode, tb=False):
+def _run_sdd(A, B, Cm, cv, mode, tb=False, ta=False):
     cv.fill_(float("nan"))
     prev = sp.select_dsd_kernel(mode)
     try:
-        sp.Matmul(A, False, B, tb, Cm)
+        sp.Matmul(A, ta, B, tb, Cm)
         torch.cuda.synchronize()
     finally:
         sp.select_dsd_kernel(prev)
@@ -268,23 +269,26 @@ SDD_CASES = [
 
 @pytest.mark.parametrize("m,k,n,density,uniform", SDD_CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("tb", [False, True])
-def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, tb):
-    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, density, dtype,
-                                                seed=m + k + n, uniform=uniform, tb=tb)
-    c4 = _run_sdd(A, B, Cm, cv, 1, tb)
-    c8 = _run_sdd(A, B, Cm, cv, 0, tb)
+@pytest.mark.parametrize("trans", ["NN", "NT", "TT"])
+def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, trans):
+    ta, tb = trans[0] == "T", trans[1] == "T"
+    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, density, dtype, seed=m + k + n,
+                                                uniform=uniform, tb=tb, ta=ta)
+    c4 = _run_sdd(A, B, Cm, cv, 1, tb, ta)
+    c8 = _run_sdd(A, B, Cm, cv, 0, tb, ta)
     assert not torch.isnan(c4.float()).any()
     assert torch.equal(c4, c8), (
         f"max diff {float((c4.float() - c8.float()).abs().max())}")
 
 
-@pytest.mark.parametrize("tb", [False, True])
-def test_sdd4w_oracle(tb):
+@pytest.mark.parametrize("trans", ["NN", "NT", "TT"])
+def test_sdd4w_oracle(trans):
+    ta, tb = trans[0] == "T", trans[1] == "T"
     m, k, n = 8192, 1024, 8192
-    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, 0.5, "f16", seed=11, tb=tb)
-    c4 = _run_sdd(A, B, Cm, cv, 1, tb).view(-1, 128, 128).float().cpu().numpy()
-    av = a.float().cpu().numpy().reshape(m, k)
+    A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, 0.5, "f16", seed=11, tb=tb, ta=ta)
+    c4 = _run_sdd(A, B, Cm, cv, 1, tb, ta).view(-1, 128, 128).float().cpu().numpy()
+    av = a.float().cpu().numpy().reshape(k, m).T if ta else \
+        a.float().cpu().numpy().reshape(m, k)
     bv = b.float().cpu().numpy().reshape(n, k).T if tb else \
         b.float().cpu().numpy().reshape(k, n)
     rows = np.repeat(np.arange(m // 128), np.diff(off))
