@@ -56,8 +56,8 @@ def main():
             torch.cuda.synchronize()
             return s.elapsed_time(e) * 1e3 / a.calls
 
-        arms = ({"8wave": 0, "4wave": 1} if a.op == "sdd"
-                else {"8wave": 0, "4wave": 3, "4wave_ds": 5})
+        arms = ({"8wave": 0, "4wave": 5, "4wave_bar2": 6} if a.op == "sdd"
+                else {"8wave": 0, "4wave_ds": 5, "4wave_bar2": 6})
         for mode in arms.values():
             timed(mode)
             for _ in range(100):

@@ -391,14 +391,14 @@ static int Dsd4wMode() {
   if (v < 0) {
     const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
     v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 5 ? 5 : v);
+    v = v < 0 ? 1 : (v > 6 ? 6 : v);
     g_dsd4w.store(v, std::memory_order_relaxed);
   }
   return v;
 }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2..5: wherever the kernel can run, whatever the density (tests, A/B), with
-// epilogue 0 / 1 / 2 / 3 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
+// 2..6: wherever the kernel can run, whatever the density (tests, A/B), with
+// epilogue 0 / 1 / 2 / 3 / 4 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
 bool Dsd4wForced() { return Dsd4wMode() >= 2; }
 int Dsd4wEpi() {
   const int m = Dsd4wMode();
@@ -407,7 +407,7 @@ int Dsd4wEpi() {
 int SelectDsdKernel(int four_wave) {
   const int prev = Dsd4wMode();
   if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 5 ? 5 : four_wave, std::memory_order_relaxed);
+    g_dsd4w.store(four_wave > 6 ? 6 : four_wave, std::memory_order_relaxed);
   return prev;
 }
 
@@ -937,7 +937,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   p.debug = g_debug;
   const bool grouped = UseGroupedSdd(&p, c, tb);
   if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb))
-    return LaunchSdd4w(dtype, p, ta, tb, stream);
+    return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
                          grouped, p, stream);
 }

@@ -25,7 +25,8 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 // every wave stages and stores its own 128 x 128 block (no barrier); 2 the
 // same with the last block specialized (no dummy DMA / reads, conversion
 // inside the final step's MFMAs); 3 the per-wave epilogue with the
-// k-contiguous image in double slots of 128-B row pieces (gen_dsd4w.py).
+// k-contiguous image in double slots of 128-B row pieces (gen_dsd4w.py); 4
+// the same with one barrier every other step.
 hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, hipStream_t stream);
 // The per-wave epilogue: DSD 4096^3 same-process A/B (r04b, us) 8-wave /
 // 4-wave workgroup epilogue / per-wave: 50% 63.5 / 61.2 / 60.6, 10% 27.4 /
@@ -48,7 +49,7 @@ hipError_t LaunchDds4w(int dtype, const GemmParams &p, int epi, hipStream_t stre
 // blocks of a block-row per workgroup, grid = the group count's upper
 // bound), K a multiple of 128: dsd4w.hip kSdd / kNt / kTt.
 bool Sdd4wApplies(const GemmParams &p, bool grouped, bool ta, bool tb);
-hipError_t LaunchSdd4w(int dtype, const GemmParams &p, bool ta, bool tb,
+hipError_t LaunchSdd4w(int dtype, const GemmParams &p, bool ta, bool tb, int epi,
                        hipStream_t stream);
 
 }  // namespace sputnik_amd

@@ -110,7 +110,15 @@ def dmas(slot):
 # DDS (`VARIANT["dds"]`, see build): the shared image is the sparse block's
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
-VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False}
+VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
+           "bar2": False}
+# "bar2" (double-slot mode with a double-slot SHARED image: DSD, SDD NN / NT):
+# one s_barrier every other step. The shared double slot of steps (S0, S0 +
+# 1) is first read in step S0 - 1 (odd), after that step's barrier (every
+# wave's DMA of it waited before); its second half is read in step S0 from
+# the same, already synchronized slot; it is refilled after the barrier of
+# step S0 + 1 (odd), which no wave passes before every wave has finished
+# step S0. The wave's own images need no barrier.
 # SDD TT ("tt", with "sdd" and "ds"): A stored [k][m], so the shared image is
 # the per-step [32 k][128 m] slice of A (rows lda apart: %[s16] = 4 lda
 # between its two DMAs, S advances %[sk32] = 32 lda per step and %[sk128] per
@@ -361,7 +369,8 @@ def step_ds(dt, H, zero_c=False):
     for i, ins in enumerate(own):
         gaps[READS_AT + i].append(ins)
     bar = READS_AT + len(own)
-    gaps[bar].append("s_barrier")
+    if not (VARIANT["bar2"] and not dds and not VARIANT["tt"] and H % 2 == 0):
+        gaps[bar].append("s_barrier")
     for i, ins in enumerate(shared):
         gaps[bar + 1 + i].append(ins)
     fed = (H + 3) % 4
@@ -555,6 +564,35 @@ def epilogue_body(cvt, mode, wave_epi=False):
     return out
 
 
+def epilogue_plain_interleaved(cvt):
+    """Per-wave plain epilogue with the copy-out interleaved: after the 8
+    tiles of row tile m are converted and staged, the wave reads rows 16 m ..
+    16 m + 15 back (into v[128:159], free after the k-loop, two alternating
+    sets) and stores them, so the stores of batch m drain while batch m + 1
+    converts."""
+    out = ["s_mov_b32 s84, %[cdlo]", "s_mov_b32 s85, %[cdhi]",
+           "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
+           "s_mov_b32 s78, 0"]
+    for m in range(8):
+        for n in range(8):
+            i = 8 * m + n
+            t = 96 + 8 * (i % 4)
+            out += [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
+            out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}",
+                    f"ds_write_b64 %[vws{n}], v[{t + 4}:{t + 5}] offset:{4096 * m}"]
+        base = 128 + 16 * (m % 2)
+        for j in range(4):
+            out.append(f"ds_read_b128 v[{base + 4 * j}:{base + 4 * j + 3}], "
+                       f"%[vrb{j}] offset:{4096 * m}")
+        out.append("s_waitcnt lgkmcnt(0)")
+        for j in range(4):
+            out += [f"buffer_store_dwordx4 v[{base + 4 * j}:{base + 4 * j + 3}], %[vco], "
+                    f"s[84:87], s78 offen nt",
+                    "s_add_u32 s78, s78, %[c4]"]
+        out.append("s_nop 1")
+    return out
+
+
 def copy_out():
     """Per-wave epilogue: the wave's staged 128 x 128 block -> C with 16-byte
     nontemporal buffer stores, 4 rows x 256 B per instruction (lane l: row
@@ -608,12 +646,12 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False):
-    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt)
+          sdd=False, nt=False, tt=False, bar2=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False)
+        VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -677,8 +715,14 @@ def _build(dt, wave_epi, last_block, stamps):
         # for the staging image
         body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
     body += ["s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc1 L_collect_%="]
-    body += epilogue_body(cvt, "plain", wave_epi)
-    body.append("s_branch L_done_%=")
+    if VARIANT["bar2"]:
+        # (with bar2: the plain epilogue stores each 16-row batch as soon as
+        # its 8 tiles are staged)
+        body += epilogue_plain_interleaved(cvt)
+        body.append("s_branch L_end_%=")
+    else:
+        body += epilogue_body(cvt, "plain", wave_epi)
+        body.append("s_branch L_done_%=")
     body.append("L_collect_%=:")
     body += poll()
     body.append("L_got_%=:")
@@ -688,6 +732,8 @@ def _build(dt, wave_epi, last_block, stamps):
     body += epilogue_body(cvt, "nan", wave_epi)
     body += ["L_done_%=:"]
     body += copy_out() if wave_epi else ["s_waitcnt lgkmcnt(0)"]
+    if VARIANT["bar2"]:
+        body.append("L_end_%=:")
     if stamps:
         body += ["s_memrealtime %[r2]", "s_waitcnt lgkmcnt(0)"]
     return body
@@ -717,6 +763,14 @@ def render():
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
+            lines += ['  ""', ""]
+        # _W3*: double slots with a barrier every other step
+        for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
+                              ("_W3_SDD_NT", True, True)):
+            lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
+            lines += [f'  "{ins}\\n" \\'
+                      for ins in build(dt, True, False, False, False, True, sdd, nt,
+                                       False, True)]
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]

@@ -50,7 +50,8 @@ def _problem(m, k, n, density, dtype, seed, empty_rows=()):
 def _run(A, B, m, n, dtype, mode):
     """mode: 0 the 8-wave kernel, 2 the 4-wave kernel (workgroup epilogue),
     3 with the per-wave epilogue, 4 per-wave + specialized last block, 5
-    per-wave + double-slot S image; 2-5 regardless of the density gate."""
+    per-wave + double-slot S image, 6 the same with a barrier every other
+    step; 2-6 regardless of the density gate."""
     td = torch.float16 if dtype == "f16" else torch.bfloat16
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
     prev = sp.select_dsd_kernel(mode)
@@ -78,7 +79,7 @@ CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("mode", [2, 3, 4, 5])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6])
 def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
     c4 = _run(A, B, m, n, dtype, mode)
@@ -89,7 +90,7 @@ def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     assert sp.pair_errors() == 0
 
 
-@pytest.mark.parametrize("mode", [2, 3, 4, 5])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6])
 def test_dsd4w_empty_rows_and_oracle(mode):
     """Empty block-rows get zero tiles; sampled rows against the oracle."""
     m, k, n = 4096, 2048, 1024
@@ -114,7 +115,7 @@ def test_dsd4w_empty_rows_and_oracle(mode):
 
 def test_dsd4w_selector_roundtrip():
     prev = sp.select_dsd_kernel(-1)
-    assert prev in (0, 1, 2, 3, 4, 5)
+    assert prev in (0, 1, 2, 3, 4, 5, 6)
     assert sp.select_dsd_kernel(0) == prev
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0
@@ -270,11 +271,13 @@ SDD_CASES = [
 @pytest.mark.parametrize("m,k,n,density,uniform", SDD_CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
 @pytest.mark.parametrize("trans", ["NN", "NT", "TT"])
-def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, trans):
+@pytest.mark.parametrize("mode", [5, 6])
+def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, trans, mode):
+    """mode 5: double slots; 6: and a barrier every other step (NN / NT)."""
     ta, tb = trans[0] == "T", trans[1] == "T"
     A, B, Cm, cv, off, idx, a, b = _sdd_problem(m, k, n, density, dtype, seed=m + k + n,
                                                 uniform=uniform, tb=tb, ta=ta)
-    c4 = _run_sdd(A, B, Cm, cv, 1, tb, ta)
+    c4 = _run_sdd(A, B, Cm, cv, mode, tb, ta)
     c8 = _run_sdd(A, B, Cm, cv, 0, tb, ta)
     assert not torch.isnan(c4.float()).any()
     assert torch.equal(c4, c8), (
