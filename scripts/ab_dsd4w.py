@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--calls", type=int, default=50)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--dim", type=int, default=4096)
-    ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"],
+    ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"],  # (--trans: OpProblem)
                     help="dds / sdd: bench.py's OpProblem DDS NN / SDD NN")
     ap.add_argument("--trans", default="NN")
     a = ap.parse_args()
@@ -37,7 +37,7 @@ def main():
         rng = np.random.default_rng(1)
         nz = mu.nonzeros_for_density(d, d, dens)
         off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
-        if a.op in ("dds", "sdd"):
+        if a.op in ("dds", "sdd") or a.trans != "NN":
             ns = argparse.Namespace(op=a.op, trans=a.trans, api="ex", k=d,
                                     density=dens, dtype=a.dtype, seed=0)
             prob = bench.OpProblem(ns, dev)

@@ -125,8 +125,8 @@ VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
 # k-block), read transposed into the MFMA's B-operand set; B stored [n][k]:
 # the wave's image in double slots as in NT. The DDS ring structure with the
 # operand sets exchanged.
-# SDD NT ("nt", with "sdd" and "ds"): B stored [n][k], so the wave's image is
-# k-contiguous too: both images in double slots, both read with ds_read_b128
+# SDD NT / DSD NT ("nt", with "ds"; SDD also "sdd"): B stored [n][k], so the
+# wave's image is k-contiguous too: both images in double slots, both read with ds_read_b128
 # (the wave's B rows into the MFMA's A-operand set, %[vrk0] / %[vrk1] =
 # half-0 / half-1 addresses), and every DMA is a double-slot one, on odd
 # steps.
@@ -759,7 +759,8 @@ def render():
                                            ("_W2_DDS", True, True, False, False, False),
                                            ("_W2_SDD", False, True, True, False, False),
                                            ("_W2_SDD_NT", False, True, True, True, False),
-                                           ("_W2_SDD_TT", False, True, True, False, True)):
+                                           ("_W2_SDD_TT", False, True, True, False, True),
+                                           ("_W2_NT", False, True, False, True, False)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]

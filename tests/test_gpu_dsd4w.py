@@ -47,7 +47,7 @@ def _problem(m, k, n, density, dtype, seed, empty_rows=()):
     return A, sp.Matrix(k, n, b), off, idx, a, b
 
 
-def _run(A, B, m, n, dtype, mode):
+def _run(A, B, m, n, dtype, mode, tb=False):
     """mode: 0 the 8-wave kernel, 2 the 4-wave kernel (workgroup epilogue),
     3 with the per-wave epilogue, 4 per-wave + specialized last block, 5
     per-wave + double-slot S image, 6 the same with a barrier every other
@@ -56,7 +56,7 @@ def _run(A, B, m, n, dtype, mode):
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
     prev = sp.select_dsd_kernel(mode)
     try:
-        sp.MatmulEx(A, False, B, False, sp.Matrix(m, n, c))
+        sp.MatmulEx(A, False, B, tb, sp.Matrix(m, n, c))
         torch.cuda.synchronize()
     finally:
         sp.select_dsd_kernel(prev)
@@ -300,3 +300,37 @@ def test_sdd4w_oracle(trans):
         ref = O.gemm(av[r * 128:(r + 1) * 128], False, bv[:, c * 128:(c + 1) * 128],
                      False, threads=H.oracle_threads())
         H.assert_close(c4[e], ref, "f16", f"sdd4w block {e}")
+
+
+# ----------------------------------------------------------------- DSD NT --
+# B stored [n][k] (MegaBlocks' dx = dh . w1^T): both images k-contiguous in
+# double slots (gen_dsd4w.py "nt" without "sdd").
+NT_CASES = [c for c in CASES if c[2] % 128 == 0]
+
+
+@pytest.mark.parametrize("m,k,n,density", NT_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dsd4w_nt_bit_identical_to_8wave(m, k, n, density, dtype):
+    A, _, off, idx, a, _ = _problem(m, k, n, density, dtype, seed=m + 2 * n + int(density * 100))
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(m + n)
+    bt = (torch.rand(n * k, generator=g, device="cuda") * 2 - 1).to(td)
+    Bt = sp.Matrix(n, k, bt)
+    c4 = _run(A, Bt, m, n, dtype, 5, tb=True)
+    c8 = _run(A, Bt, m, n, dtype, 0, tb=True)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+    if (m, k, n) == (2048, 4096, 4096):
+        av = a.float().cpu().numpy().reshape(-1, 128, 128)
+        bv = bt.float().cpu().numpy().reshape(n, k)
+        for r in (0, 9):
+            o0, o1 = int(off[r]), int(off[r + 1])
+            row = np.zeros((128, k), np.float32)
+            for e in range(o0, o1):
+                row[:, idx[e] * 128:(idx[e] + 1) * 128] = av[e]
+            ref = O.gemm(row, False, bv, True, threads=H.oracle_threads())
+            H.assert_close(c4[r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
+                           "f16" if dtype == "f16" else "bf16", f"dsd4w NT row-block {r}")
