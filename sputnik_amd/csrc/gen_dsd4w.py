@@ -135,6 +135,13 @@ VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
 # block; the 16-row soffset is 16 lda (%[s16]).
 
 
+def col_order():
+    """DDS in column order (B's transposed metadata: storage block per entry
+    through s_block_offsets); DDS NT reads B's rows in storage order like
+    DSD."""
+    return VARIANT["dds"] and not VARIANT["nt"]
+
+
 def s_block_shift():
     """(high, low) shifts of S's byte offset from the entry in s76."""
     return (24, 8) if VARIANT["sdd"] else (17, 15)
@@ -160,7 +167,7 @@ def entry_of(xreg, out_reg):
 # (DDS: the S block is the storage block of the entry, s_block_offsets[e],
 # kept in s63 and prefetched into s62 like the k-block.)
 def switch():
-    if VARIANT["dds"]:
+    if col_order():
         blk = ["s_lshr_b32 s77, s63, 17", "s_lshl_b32 s76, s63, 15"]
     elif VARIANT["tt"]:
         blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
@@ -175,7 +182,7 @@ def switch():
                  "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
                  "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
                  "s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"]
-    if VARIANT["dds"]:
+    if col_order():
         out.append("s_mov_b32 s63, s62")
     return out
 
@@ -185,7 +192,7 @@ def idx_load():
     if VARIANT["sdd"]:  # k-block of virtual entry x is x
         return ["s_min_u32 s59, s56, %[xlast]", "s_add_u32 s56, s56, 1", "s_mov_b32 s60, 0"]
     out = ["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"] + entry_of("s78", "s79")
-    if VARIANT["dds"]:
+    if col_order():
         out += ["s_lshl_b32 s74, s79, 2", "s_add_u32 s74, %[bolo], s74",
                 "s_addc_u32 s75, %[bohi], 0", "s_load_dword s62, s[74:75], 0x0"]
     return out + ["s_lshl_b32 s79, s79, 1", "s_and_b32 s60, s79, 2",
@@ -290,7 +297,7 @@ def ds_dmas(d):
     %[vs<q>], soffset p x 16 rows), DDS the wave's 128 rows of A (rows 16 p +
     8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows). (SDD NT: the
     shared one here, the wave's own in own_ds_dmas.)"""
-    if VARIANT["dds"] or VARIANT["tt"]:
+    if col_order() or VARIANT["tt"]:
         return own_ds_dmas(d)
     return [(f"s_add_u32 m0, %[ms], {d * DS_SLOT + (2 * p + q) * 1024}",
              f"buffer_load_dwordx4 {'%[vs]' if q == 0 else '%[vs1]'}, s[40:43], "
@@ -361,6 +368,9 @@ def step_ds(dt, H, zero_c=False):
     kc = s_reads_ds(s1 // 2, s1 % 2, nxt)
     if VARIANT["nt"]:
         own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), kc
+        if dds:  # DDS NT: A operand (FD) from the shared image (B's rows,
+            # %[vrk*]), B operand (FS) from the wave's rows of A (%[vrs*])
+            own, shared = shared, own
     elif VARIANT["tt"]:
         own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), d_reads(s1, nxt, FS)
     else:
@@ -473,12 +483,12 @@ def prologue_setup():
            "s_mov_b32 s56, 2", "s_mov_b32 s57, 0",
            "s_mov_b32 s58, %[kb1]", "s_mov_b32 s61, %[ntot]",
            "s_mov_b32 s72, " + ("%[s16]" if VARIANT["sdd"] else
-                                f"{1024 if VARIANT['dds'] else 4096}"),
+                                f"{1024 if col_order() else 4096}"),
            "s_mov_b32 s64, 0"]
     out += [f"s_mul_i32 s{64 + q}, %[k4], {q}" for q in range(1, 8)]
     # block 0: virtual entry 0, k-block kb0 (DDS: storage block bo0; s63 =
     # entry 1's, bo1)
-    if VARIANT["dds"]:
+    if col_order():
         out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
                 "s_mov_b32 s63, %[bo1]"]
     elif VARIANT["tt"]:  # entry 0: the panel's first k-block
@@ -760,7 +770,8 @@ def render():
                                            ("_W2_SDD", False, True, True, False, False),
                                            ("_W2_SDD_NT", False, True, True, True, False),
                                            ("_W2_SDD_TT", False, True, True, False, True),
-                                           ("_W2_NT", False, True, False, True, False)):
+                                           ("_W2_NT", False, True, False, True, False),
+                                           ("_W2_DDS_NT", True, True, False, True, False)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
