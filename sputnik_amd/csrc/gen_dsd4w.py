@@ -84,6 +84,18 @@ def d_reads(slot, s, into=None):
     return out
 
 
+def t_reads(slot, s):
+    """DSD TN: the 8 row-tile fragments, transposed, from the shared [32 k]
+    [128 m] slice into the B-operand set."""
+    out = []
+    for m in range(8):
+        b = FS[s] + 4 * m
+        out.append(f"ds_read_b64_tr_b16 v[{b}:{b + 1}], %[vrt{m}] offset:{slot * SLOT}")
+        out.append(f"ds_read_b64_tr_b16 v[{b + 2}:{b + 3}], %[vrt{m}] "
+                   f"offset:{slot * SLOT + 1024}")
+    return out
+
+
 def s_reads(slot, s):
     return [f"ds_read_b128 v[{FS[s] + 4 * m}:{FS[s] + 4 * m + 3}], %[vrs] "
             f"offset:{slot * SLOT + m * 1024}" for m in range(8)]
@@ -111,7 +123,11 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False}
+           "bar2": False, "tn": False}
+# DSD TN ("tn", per-step images): A^T in column order (A's transposed
+# metadata), so the shared image is the sparse block's [32 k][128 m] slice as
+# in DDS, read transposed into the B-operand set (%[vrt<m>]); B's [32 k][128
+# n] slice per wave as in DSD NN.
 # "bar2" (double-slot mode with a double-slot SHARED image: DSD, SDD NN / NT):
 # one s_barrier every other step. The shared double slot of steps (S0, S0 +
 # 1) is first read in step S0 - 1 (odd), after that step's barrier (every
@@ -136,10 +152,10 @@ VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
 
 
 def col_order():
-    """DDS in column order (B's transposed metadata: storage block per entry
-    through s_block_offsets); DDS NT reads B's rows in storage order like
-    DSD."""
-    return VARIANT["dds"] and not VARIANT["nt"]
+    """DDS / DSD TN in column order (the sparse operand's transposed
+    metadata: storage block per entry through s_block_offsets); DDS NT reads
+    B's rows in storage order like DSD."""
+    return (VARIANT["dds"] and not VARIANT["nt"]) or VARIANT["tn"]
 
 
 def s_block_shift():
@@ -148,7 +164,7 @@ def s_block_shift():
 
 
 def advance():
-    s = 8192 if VARIANT["dds"] else 64
+    s = 8192 if VARIANT["dds"] or VARIANT["tn"] else 64
     return [f"s_add_u32 s40, s40, {s}", "s_addc_u32 s41, s41, 0",
             "s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
 
@@ -230,6 +246,8 @@ def step(dt, H, zero_c=False, last=0, cvt=None):
         own, shared = d_reads((H + 1) % 4, nxt), s_reads((H + 1) % 4, nxt)
         if VARIANT["dds"]:
             own, shared = shared, own
+        if VARIANT["tn"]:
+            shared = t_reads((H + 1) % 4, nxt)
         for i, ins in enumerate(own):
             gaps[READS_AT + i].append(ins)
         # every wave's S DMA of step + 1 landed (each waited above) / every
@@ -466,7 +484,7 @@ def prologue():
         out += advance()
     # (no accumulator zeroing: the first step's MFMAs take C = 0)
     out += ["s_waitcnt vmcnt(10)", "s_barrier"]
-    out += d_reads(0, 0) + s_reads(0, 0)
+    out += d_reads(0, 0) + (t_reads(0, 0) if VARIANT["tn"] else s_reads(0, 0))
     for m0, ld in dmas(2):
         out += [m0, "s_nop 0", ld]
     out += advance()
@@ -656,12 +674,13 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False, bar2=False):
-    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2)
+          sdd=False, nt=False, tt=False, bar2=False, tn=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
-        VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False)
+        VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
+                       tn=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -776,6 +795,10 @@ def render():
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
             lines += ['  ""', ""]
+        # DSD TN (per-step images, per-wave epilogue)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_TN \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, tn=True)]
+        lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
                               ("_W3_SDD_NT", True, True)):

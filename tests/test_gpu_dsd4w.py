@@ -384,3 +384,60 @@ def test_dds4w_nt_bit_identical_to_8wave(m, k, n, density, dtype):
             ref = O.gemm(av, False, blk, True, threads=H.oracle_threads())
             H.assert_close(c4[:, r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
                            "f16" if dtype == "f16" else "bf16", f"dds4w NT col {r}")
+
+
+# ----------------------------------------------------------------- DSD TN --
+# C = A^T . B, A sparse [k][m] through its transposed metadata (MegaBlocks'
+# dw2 = h^T . dy): the shared image is the stored block's k-row slice, read
+# transposed (dsd4w.hip kTn).
+TN_CASES = [
+    # m (= A's columns), k (= A's rows), n, density
+    (4096, 4096, 4096, 0.5),
+    (4096, 4096, 4096, 0.1),
+    (4096, 4096, 4096, 0.9),
+    (2048, 4096, 4096, 0.3),
+    (4096, 2048, 1032, 0.5),
+    (8192, 2048, 2048, 0.3),
+]
+
+
+@pytest.mark.parametrize("m,k,n,density", TN_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dsd4w_tn_bit_identical_to_8wave(m, k, n, density, dtype):
+    At, B, off, idx, a, b = _problem(k, m, n, density, dtype, seed=m + 5 * n + int(density * 10))
+    # _problem built A as [k][m] (its k-dim = m here) and B as [m][n]; B must
+    # be [k][n]
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(m * 3 + n)
+    bb = (torch.rand(k * n, generator=g, device="cuda") * 2 - 1).to(td)
+    Bm = sp.Matrix(k, n, bb)
+    sp.AllocateTransposeBuffers(At)
+    sp.Transpose(At)
+
+    def run(mode):
+        c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+        prev = sp.select_dsd_kernel(mode)
+        try:
+            sp.MatmulEx(At, True, Bm, False, sp.Matrix(m, n, c))
+            torch.cuda.synchronize()
+        finally:
+            sp.select_dsd_kernel(prev)
+        return c.view(m, n)
+
+    c4, c8 = run(1), run(0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+    if (m, k, n, density) == (2048, 4096, 4096, 0.3):
+        av = a.float().cpu().numpy().reshape(-1, 128, 128)
+        dense_a = np.zeros((k, m), np.float32)
+        rows = np.repeat(np.arange(k // 128), np.diff(off))
+        for e in range(int(off[-1])):
+            r, c = int(rows[e]), int(idx[e])
+            dense_a[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128] = av[e]
+        bv = bb.float().cpu().numpy().reshape(k, n)
+        ref = O.gemm(dense_a[:, :256], True, bv, False, threads=H.oracle_threads())
+        H.assert_close(c4[:256].float().cpu().numpy(), ref,
+                       "f16" if dtype == "f16" else "bf16", "dsd4w TN rows 0..255")
