@@ -246,7 +246,12 @@ def step(dt, H, zero_c=False, last=0, cvt=None):
         own, shared = d_reads((H + 1) % 4, nxt), s_reads((H + 1) % 4, nxt)
         if VARIANT["dds"]:
             own, shared = shared, own
-        if VARIANT["tn"]:
+        if VARIANT["tn"] and VARIANT["dds"]:
+            # DDS TN: A^T's [32 k][128 m] slice per wave, read transposed
+            # into the B operand (%[vrt<m>] on the wave's own ring); the
+            # shared sparse slice into the A operand as in DDS NN
+            own, shared = t_reads((H + 1) % 4, nxt), d_reads((H + 1) % 4, nxt)
+        elif VARIANT["tn"]:
             shared = t_reads((H + 1) % 4, nxt)
         for i, ins in enumerate(own):
             gaps[READS_AT + i].append(ins)
@@ -795,10 +800,11 @@ def render():
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
             lines += ['  ""', ""]
-        # DSD TN (per-step images, per-wave epilogue)
-        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W_TN \\")
-        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, tn=True)]
-        lines += ['  ""', ""]
+        # DSD TN and DDS TN (per-step images, per-wave epilogue)
+        for name, dds in (("_W_TN", False), ("_W_DDS_TN", True)):
+            lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
+            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, dds=dds, tn=True)]
+            lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
                               ("_W3_SDD_NT", True, True)):

@@ -441,3 +441,44 @@ def test_dsd4w_tn_bit_identical_to_8wave(m, k, n, density, dtype):
         ref = O.gemm(dense_a[:, :256], True, bv, False, threads=H.oracle_threads())
         H.assert_close(c4[:256].float().cpu().numpy(), ref,
                        "f16" if dtype == "f16" else "bf16", "dsd4w TN rows 0..255")
+
+
+# ----------------------------------------------------------------- DDS TN --
+# C = A^T . B, A stored [k][m] (MegaBlocks' dw1 = x^T . dh's shape): A's
+# k-row slices per wave, read transposed (dsd4w.hip kDds + kTn).
+
+@pytest.mark.parametrize("m,k,n,density", DDS_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dds4w_tn_bit_identical_to_8wave(m, k, n, density, dtype):
+    _, B, off, idx, a, b = _dds_problem(m, k, n, density, dtype,
+                                        seed=2 * m + n + int(density * 100))
+    At = sp.Matrix(k, m, a)  # the same m * k values, stored [k][m]
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+
+    def run(mode):
+        c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+        prev = sp.select_dsd_kernel(mode)
+        try:
+            sp.MatmulEx(At, True, B, False, sp.Matrix(m, n, c))
+            torch.cuda.synchronize()
+        finally:
+            sp.select_dsd_kernel(prev)
+        return c.view(m, n)
+
+    c4, c8 = run(1), run(0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+    if (m, k, n) == (1152, 2048, 2048):
+        av = a.float().cpu().numpy().reshape(k, m)
+        bv = b.float().cpu().numpy().reshape(-1, 128, 128)
+        rows = np.repeat(np.arange(k // 128), np.diff(off))
+        for c in (0, 9):
+            col = np.zeros((k, 128), np.float32)
+            for e in np.nonzero(idx == c)[0]:
+                r = int(rows[e])
+                col[r * 128:(r + 1) * 128] = bv[e]
+            ref = O.gemm(av, True, col, False, threads=H.oracle_threads())
+            H.assert_close(c4[:, c * 128:(c + 1) * 128].float().cpu().numpy(), ref,
+                           "f16" if dtype == "f16" else "bf16", f"dds4w TN col {c}")
