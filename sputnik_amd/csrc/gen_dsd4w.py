@@ -155,7 +155,13 @@ def col_order():
     """DDS / DSD TN in column order (the sparse operand's transposed
     metadata: storage block per entry through s_block_offsets); DDS NT reads
     B's rows in storage order like DSD."""
-    return (VARIANT["dds"] and not VARIANT["nt"]) or VARIANT["tn"]
+    return (VARIANT["dds"] and not VARIANT["nt"]) or (VARIANT["tn"] and not VARIANT["sdd"])
+
+
+def a_rows_t():
+    """SDD TT / TN: the shared image is A's [32 k][128 m] slice (rows lda
+    apart): S advances %[sk32] per step and %[sk128] per k-block."""
+    return VARIANT["tt"] or (VARIANT["tn"] and VARIANT["sdd"])
 
 
 def s_block_shift():
@@ -164,7 +170,8 @@ def s_block_shift():
 
 
 def advance():
-    s = 8192 if VARIANT["dds"] or VARIANT["tn"] else 64
+    s = ("%[sk32]" if a_rows_t() else
+         8192 if VARIANT["dds"] or VARIANT["tn"] else 64)
     return [f"s_add_u32 s40, s40, {s}", "s_addc_u32 s41, s41, 0",
             "s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
 
@@ -185,7 +192,7 @@ def entry_of(xreg, out_reg):
 def switch():
     if col_order():
         blk = ["s_lshr_b32 s77, s63, 17", "s_lshl_b32 s76, s63, 15"]
-    elif VARIANT["tt"]:
+    elif a_rows_t():
         blk = (["s_add_u32 s57, s57, 1", "s_min_u32 s57, s57, %[xlast]"]
                + entry_of("s57", "s78")
                + ["s_mul_hi_u32 s77, s78, %[sk128]", "s_mul_i32 s76, s78, %[sk128]"])
@@ -514,7 +521,7 @@ def prologue_setup():
     if col_order():
         out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
                 "s_mov_b32 s63, %[bo1]"]
-    elif VARIANT["tt"]:  # entry 0: the panel's first k-block
+    elif a_rows_t():  # entry 0: the panel's first k-block
         out += ["s_mov_b32 s76, 0", "s_mov_b32 s77, 0"]
     else:
         hi, lo = s_block_shift()
@@ -800,10 +807,12 @@ def render():
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
             lines += ['  ""', ""]
-        # DSD TN and DDS TN (per-step images, per-wave epilogue)
-        for name, dds in (("_W_TN", False), ("_W_DDS_TN", True)):
+        # DSD / DDS / SDD TN (per-step images, per-wave epilogue)
+        for name, dds, sdd in (("_W_TN", False, False), ("_W_DDS_TN", True, False),
+                               ("_W_SDD_TN", False, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
-            lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, dds=dds, tn=True)]
+            lines += [f'  "{ins}\\n" \\'
+                      for ins in build(dt, True, dds=dds, sdd=sdd, tn=True)]
             lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),

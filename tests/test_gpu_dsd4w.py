@@ -270,7 +270,7 @@ SDD_CASES = [
 
 @pytest.mark.parametrize("m,k,n,density,uniform", SDD_CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("trans", ["NN", "NT", "TT"])
+@pytest.mark.parametrize("trans", ["NN", "NT", "TN", "TT"])
 @pytest.mark.parametrize("mode", [5, 6])
 def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, trans, mode):
     """mode 5: double slots; 6: and a barrier every other step (NN / NT)."""
@@ -284,7 +284,7 @@ def test_sdd4w_bit_identical_to_8wave(m, k, n, density, uniform, dtype, trans, m
         f"max diff {float((c4.float() - c8.float()).abs().max())}")
 
 
-@pytest.mark.parametrize("trans", ["NN", "NT", "TT"])
+@pytest.mark.parametrize("trans", ["NN", "NT", "TN", "TT"])
 def test_sdd4w_oracle(trans):
     ta, tb = trans[0] == "T", trans[1] == "T"
     m, k, n = 8192, 1024, 8192
