@@ -893,7 +893,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall))
-    return LaunchDsd4w(dtype, p, Dsd4wEpi(), tb, stream, ta && !tb);
+    return LaunchDsd4w(dtype, p, Dsd4wEpi(), tb && !ta, stream, ta && !tb, ta && tb);
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 

@@ -11,7 +11,7 @@ namespace sputnik_amd {
 // Whether the 4-wave kernel serves this prepared launch: DSD with S
 // k-contiguous (A not transposed) and D n-contiguous (B not transposed) or
 // k-contiguous (NT: B stored [n][k], N a multiple of 128), or A transposed
-// through its column-order metadata with B not transposed (TN),
+// through its column-order metadata (TN, TT),
 // straight output, on the one-tile-per-CU 128 x 512 launch (plain or pair
 // balanced; not split mode, not persistent, not the tall configuration).
 // blocks: stored blocks of the sparse operand; below a mean of
@@ -30,7 +30,7 @@ bool Dsd4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
 // k-contiguous image in double slots of 128-B row pieces (gen_dsd4w.py); 4
 // the same with one barrier every other step.
 hipError_t LaunchDsd4w(int dtype, const GemmParams &p, int epi, bool nt,
-                       hipStream_t stream, bool tn = false);
+                       hipStream_t stream, bool tn = false, bool tt = false);
 // The per-wave epilogue: DSD 4096^3 same-process A/B (r04b, us) 8-wave /
 // 4-wave workgroup epilogue / per-wave: 50% 63.5 / 61.2 / 60.6, 10% 27.4 /
 // 28.4 / 27.1, 30% 43.7 / 45.2 / 43.7, 90% 97.7 / 93.9 / 93.0; the

@@ -155,13 +155,14 @@ def col_order():
     """DDS / DSD TN in column order (the sparse operand's transposed
     metadata: storage block per entry through s_block_offsets); DDS NT reads
     B's rows in storage order like DSD."""
-    return (VARIANT["dds"] and not VARIANT["nt"]) or (VARIANT["tn"] and not VARIANT["sdd"])
+    return ((VARIANT["dds"] and not VARIANT["nt"])
+            or ((VARIANT["tn"] or VARIANT["tt"]) and not VARIANT["sdd"]))
 
 
 def a_rows_t():
     """SDD TT / TN: the shared image is A's [32 k][128 m] slice (rows lda
     apart): S advances %[sk32] per step and %[sk128] per k-block."""
-    return VARIANT["tt"] or (VARIANT["tn"] and VARIANT["sdd"])
+    return (VARIANT["tt"] or VARIANT["tn"]) and VARIANT["sdd"]
 
 
 def s_block_shift():
@@ -347,8 +348,9 @@ def s_reads_ds(d, half, s):
 def advance_per_step():
     if VARIANT["nt"]:
         return []
-    if VARIANT["tt"]:
-        return ["s_add_u32 s40, s40, %[sk32]", "s_addc_u32 s41, s41, 0"]
+    if VARIANT["tt"]:  # (DSD TT: the stored block's next 32 k-rows)
+        s = "%[sk32]" if VARIANT["sdd"] else 8192
+        return [f"s_add_u32 s40, s40, {s}", "s_addc_u32 s41, s41, 0"]
     return (["s_add_u32 s40, s40, 8192", "s_addc_u32 s41, s41, 0"] if VARIANT["dds"]
             else ["s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"])
 
@@ -802,7 +804,8 @@ def render():
                                            ("_W2_SDD_NT", False, True, True, True, False),
                                            ("_W2_SDD_TT", False, True, True, False, True),
                                            ("_W2_NT", False, True, False, True, False),
-                                           ("_W2_DDS_NT", True, True, False, True, False)):
+                                           ("_W2_DDS_NT", True, True, False, True, False),
+                                           ("_W2_TT", False, True, False, False, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]

@@ -482,3 +482,44 @@ def test_dds4w_tn_bit_identical_to_8wave(m, k, n, density, dtype):
             ref = O.gemm(av, True, col, False, threads=H.oracle_threads())
             H.assert_close(c4[:, c * 128:(c + 1) * 128].float().cpu().numpy(), ref,
                            "f16" if dtype == "f16" else "bf16", f"dds4w TN col {c}")
+
+
+# ----------------------------------------------------------------- DSD TT --
+@pytest.mark.parametrize("m,k,n,density", [c for c in TN_CASES if c[2] % 128 == 0])
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dsd4w_tt_bit_identical_to_8wave(m, k, n, density, dtype):
+    At, _, off, idx, a, _ = _problem(k, m, n, density, dtype, seed=m + 7 * n + int(density * 10))
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(m * 5 + n)
+    bt = (torch.rand(n * k, generator=g, device="cuda") * 2 - 1).to(td)
+    Bt = sp.Matrix(n, k, bt)
+    sp.AllocateTransposeBuffers(At)
+    sp.Transpose(At)
+
+    def run(mode):
+        c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+        prev = sp.select_dsd_kernel(mode)
+        try:
+            sp.MatmulEx(At, True, Bt, True, sp.Matrix(m, n, c))
+            torch.cuda.synchronize()
+        finally:
+            sp.select_dsd_kernel(prev)
+        return c.view(m, n)
+
+    c4, c8 = run(1), run(0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+    if (m, k, n, density) == (2048, 4096, 4096, 0.3):
+        av = a.float().cpu().numpy().reshape(-1, 128, 128)
+        dense_a = np.zeros((k, m), np.float32)
+        rows = np.repeat(np.arange(k // 128), np.diff(off))
+        for e in range(int(off[-1])):
+            r, c = int(rows[e]), int(idx[e])
+            dense_a[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128] = av[e]
+        bv = bt.float().cpu().numpy().reshape(n, k)
+        ref = O.gemm(dense_a[:, :256], True, bv, True, threads=H.oracle_threads())
+        H.assert_close(c4[:256].float().cpu().numpy(), ref,
+                       "f16" if dtype == "f16" else "bf16", "dsd4w TT rows 0..255")
