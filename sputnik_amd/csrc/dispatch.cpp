@@ -921,7 +921,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
       return e != nullptr ? std::atoi(e) : 0;
     }();
     if (p.pair_xcd2 != 0) p.pair_xcd2 = dds_xcd2;
-    return LaunchDds4w(dtype, p, Dsd4wEpi(), tb, stream, ta && !tb);
+    return LaunchDds4w(dtype, p, Dsd4wEpi(), tb && !ta, stream, ta && !tb, ta && tb);
   }
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);

@@ -46,11 +46,11 @@ constexpr int kDsd4wDefaultEpi = 3;
 // images swapped (dsd4w.hip kDds), per-wave epilogue; M a multiple of 128.
 // DDS NT (op(B)^T rows = B's block-rows, k-contiguous): both images in
 // double slots (kDds + kNt). DDS TN (A stored [k][m]): A's k-row slices per
-// wave, read transposed (kDds + kTn).
+// wave, read transposed (kDds + kTn). DDS TT: both (kDds + kTt).
 bool Dds4wApplies(const GemmParams &p, long long blocks, bool s_kc, bool d_kc,
                   bool out_t, bool tall);
 hipError_t LaunchDds4w(int dtype, const GemmParams &p, int epi, bool nt,
-                       hipStream_t stream, bool tn = false);
+                       hipStream_t stream, bool tn = false, bool tt = false);
 
 // Grouped SDD NN / NT / TT (dispatch.cpp UseGroupedSdd: up to 4 stored
 // blocks of a block-row per workgroup, grid = the group count's upper

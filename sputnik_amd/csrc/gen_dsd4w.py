@@ -123,7 +123,11 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False, "tn": False}
+           "bar2": False, "tn": False, "ddstt": False}
+# DDS TT ("ddstt", with "ds"): B's rows (storage order) are the shared image
+# in double slots as in DSD; A stored [k][m] gives each wave a per-step [32 k]
+# [128 m] slice as DSD's B, read transposed into the B operand (%[vrt<m>]),
+# and the shared rows go to the A operand with ds_read_b128 (%[vrk*]).
 # DSD TN ("tn", per-step images): A^T in column order (A's transposed
 # metadata), so the shared image is the sparse block's [32 k][128 m] slice as
 # in DDS, read transposed into the B-operand set (%[vrt<m>]); B's [32 k][128
@@ -155,6 +159,8 @@ def col_order():
     """DDS / DSD TN in column order (the sparse operand's transposed
     metadata: storage block per entry through s_block_offsets); DDS NT reads
     B's rows in storage order like DSD."""
+    if VARIANT["ddstt"]:
+        return False
     return ((VARIANT["dds"] and not VARIANT["nt"])
             or ((VARIANT["tn"] or VARIANT["tt"]) and not VARIANT["sdd"]))
 
@@ -307,7 +313,7 @@ def per_step_dmas(slot):
     (2 x 4 k-rows of this wave's 8); SDD NT none."""
     if VARIANT["nt"]:
         return []
-    if VARIANT["dds"] or VARIANT["tt"]:
+    if (VARIANT["dds"] or VARIANT["tt"]) and not VARIANT["ddstt"]:
         return [(f"s_add_u32 m0, %[ms], {slot * SLOT + q * 1024}",
                  f"buffer_load_dwordx4 %[vs], s[40:43], {'0' if q == 0 else 's72'} "
                  f"offen lds") for q in range(2)]
@@ -328,7 +334,7 @@ def ds_dmas(d):
     %[vs<q>], soffset p x 16 rows), DDS the wave's 128 rows of A (rows 16 p +
     8 q + l / 8: %[vd<q>], soffset s<64 + p> = p x 16 rows). (SDD NT: the
     shared one here, the wave's own in own_ds_dmas.)"""
-    if col_order() or VARIANT["tt"]:
+    if (col_order() or VARIANT["tt"]) and not VARIANT["ddstt"]:
         return own_ds_dmas(d)
     return [(f"s_add_u32 m0, %[ms], {d * DS_SLOT + (2 * p + q) * 1024}",
              f"buffer_load_dwordx4 {'%[vs]' if q == 0 else '%[vs1]'}, s[40:43], "
@@ -348,6 +354,8 @@ def s_reads_ds(d, half, s):
 def advance_per_step():
     if VARIANT["nt"]:
         return []
+    if VARIANT["ddstt"]:
+        return ["s_add_u32 s44, s44, %[k32]", "s_addc_u32 s45, s45, 0"]
     if VARIANT["tt"]:  # (DSD TT: the stored block's next 32 k-rows)
         s = "%[sk32]" if VARIANT["sdd"] else 8192
         return [f"s_add_u32 s40, s40, {s}", "s_addc_u32 s41, s41, 0"]
@@ -356,6 +364,8 @@ def advance_per_step():
 
 
 def advance_ds():
+    if VARIANT["ddstt"]:
+        return ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0"]
     if VARIANT["nt"]:
         return ["s_add_u32 s40, s40, 128", "s_addc_u32 s41, s41, 0",
                 "s_add_u32 s44, s44, 128", "s_addc_u32 s45, s45, 0"]
@@ -368,6 +378,8 @@ def ds_counts():
     """DMA instructions a wave issues in an (odd, even) step."""
     if VARIANT["nt"]:
         return (20, 0)
+    if VARIANT["ddstt"]:
+        return (12, 8)
     return (18, 2) if VARIANT["dds"] or VARIANT["tt"] else (12, 8)
 
 
@@ -398,7 +410,9 @@ def step_ds(dt, H, zero_c=False):
         gaps[1] += switch()
     s1 = (H + 1) % 4
     kc = s_reads_ds(s1 // 2, s1 % 2, nxt)
-    if VARIANT["nt"]:
+    if VARIANT["ddstt"]:
+        own, shared = t_reads(s1, nxt), own_reads_kc(s1 // 2, s1 % 2, nxt)
+    elif VARIANT["nt"]:
         own, shared = own_reads_kc(s1 // 2, s1 % 2, nxt), kc
         if dds:  # DDS NT: A operand (FD) from the shared image (B's rows,
             # %[vrk*]), B operand (FS) from the wave's rows of A (%[vrs*])
@@ -420,7 +434,7 @@ def step_ds(dt, H, zero_c=False):
         # the wave's own double slot anywhere, the shared one after the
         # barrier (gap 10)
         pos_per, pos_ds = [], [51, 54, 57, 60]
-    elif dds or VARIANT["tt"]:
+    elif (dds or VARIANT["tt"]) and not VARIANT["ddstt"]:
         pos_per, pos_ds = [3, 9], [13 + 3 * i for i in range(16)]
     else:
         pos_per, pos_ds = [3, 9, 15, 21, 27, 33, 39, 45], [30, 36, 42, 48]
@@ -462,7 +476,9 @@ def prologue_ds():
     out += issue(ds_dmas(0)) + issue(own_ds(0)) + advance_ds()
     out += issue(per_step_dmas(1)) + advance_per_step()
     out += [f"s_waitcnt vmcnt({ds_counts()[1]})", "s_barrier"]
-    if VARIANT["nt"]:
+    if VARIANT["ddstt"]:
+        out += t_reads(0, 0) + own_reads_kc(0, 0, 0)
+    elif VARIANT["nt"]:
         out += own_reads_kc(0, 0, 0) + s_reads_ds(0, 0, 0)
     elif VARIANT["tt"]:
         out += own_reads_kc(0, 0, 0) + d_reads(0, 0, FS)
@@ -688,13 +704,13 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False, bar2=False, tn=False):
-    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn)
+          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
         VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
-                       tn=False)
+                       tn=False, ddstt=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -817,6 +833,11 @@ def render():
             lines += [f'  "{ins}\\n" \\'
                       for ins in build(dt, True, dds=dds, sdd=sdd, tn=True)]
             lines += ['  ""', ""]
+        # DDS TT
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_DDS_TT \\")
+        lines += [f'  "{ins}\\n" \\'
+                  for ins in build(dt, True, dds=True, ds=True, ddstt=True)]
+        lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
                               ("_W3_SDD_NT", True, True)):

@@ -523,3 +523,50 @@ def test_dsd4w_tt_bit_identical_to_8wave(m, k, n, density, dtype):
         ref = O.gemm(dense_a[:, :256], True, bv, True, threads=H.oracle_threads())
         H.assert_close(c4[:256].float().cpu().numpy(), ref,
                        "f16" if dtype == "f16" else "bf16", "dsd4w TT rows 0..255")
+
+
+# ----------------------------------------------------------------- DDS TT --
+@pytest.mark.parametrize("m,k,n,density", DDS_CASES)
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_dds4w_tt_bit_identical_to_8wave(m, k, n, density, dtype):
+    rng = np.random.default_rng(m + 3 * n + 11)
+    R, C = n // 128, k // 128
+    nz = mu.nonzeros_for_density(n, k, density) // (128 * 128)
+    off, idx = mu.random_topology(R, C, nz, rng, unordered=True)
+    td = torch.float16 if dtype == "f16" else torch.bfloat16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(m + 2 * k)
+    nb = int(off[-1])
+    a = (torch.rand(m * k, generator=g, device="cuda") * 2 - 1).to(td)
+    b = (torch.rand(max(nb, 1) * 16384, generator=g, device="cuda") * 2 - 1).to(td)
+    B = sp.BlockMatrix(n, k, 128, nb * 16384, b,
+                       torch.from_numpy(np.asarray(off, np.int32)).cuda(),
+                       torch.from_numpy(np.asarray(idx).astype(np.int16)).cuda())
+    At = sp.Matrix(k, m, a)
+
+    def run(mode):
+        c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
+        prev = sp.select_dsd_kernel(mode)
+        try:
+            sp.MatmulEx(At, True, B, True, sp.Matrix(m, n, c))
+            torch.cuda.synchronize()
+        finally:
+            sp.select_dsd_kernel(prev)
+        return c.view(m, n)
+
+    c4, c8 = run(1), run(0)
+    assert not torch.isnan(c4.float()).any()
+    assert torch.equal(c4, c8), (
+        f"max diff {float((c4.float() - c8.float()).abs().max())}")
+    assert sp.pair_errors() == 0
+    if (m, k, n) == (1152, 2048, 2048):
+        av = a.float().cpu().numpy().reshape(k, m)
+        bv = b.float().cpu().numpy().reshape(-1, 128, 128)
+        rows = np.repeat(np.arange(R), np.diff(off))
+        for r in (0, 5):
+            blk = np.zeros((128, k), np.float32)
+            for e in np.nonzero(rows == r)[0]:
+                blk[:, idx[e] * 128:(idx[e] + 1) * 128] = bv[e]
+            ref = O.gemm(av, True, blk, True, threads=H.oracle_threads())
+            H.assert_close(c4[:, r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
+                           "f16" if dtype == "f16" else "bf16", f"dds4w TT col {r}")
