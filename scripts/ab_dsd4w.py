@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--op", default="dsd", choices=["dsd", "dds", "sdd"],  # (--trans: OpProblem)
                     help="dds / sdd: bench.py's OpProblem DDS NN / SDD NN")
     ap.add_argument("--trans", default="NN")
+    ap.add_argument("--m", type=int, default=0, help="DSD NN: rows of A (default --dim)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,13 +37,15 @@ def main():
     for dens in [float(x) for x in a.densities.split(",")]:
         rng = np.random.default_rng(1)
         nz = mu.nonzeros_for_density(d, d, dens)
-        off, idx = mu.random_topology(d // 128, d // 128, nz // 16384, rng)
+        mr = a.m or d
+        nz = mu.nonzeros_for_density(mr, d, dens)
+        off, idx = mu.random_topology(mr // 128, d // 128, nz // 16384, rng)
         if a.op in ("dds", "sdd") or a.trans != "NN":
             ns = argparse.Namespace(op=a.op, trans=a.trans, api="ex", k=d,
                                     density=dens, dtype=a.dtype, seed=0)
             prob = bench.OpProblem(ns, dev)
         else:
-            prob = bench.DsdProblem(d, d, off, idx, d, False, False, a.dtype, 7, dev)
+            prob = bench.DsdProblem(mr, d, off, idx, d, False, False, a.dtype, 7, dev)
         fn = prob.launcher()
 
         def timed(four):

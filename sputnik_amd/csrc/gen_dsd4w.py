@@ -42,7 +42,8 @@ Register map (literal, declared as clobbers):
 Everything read-only comes in as an operand (%[name]); %[flags] packs the
 workgroup's role bits: 0 collect (pair consumer), 1 specialized last block
 allowed, 2 test fault (producer skips its flag), 3 last wave (raises the
-flag), 4 wave 0 (counts a time-out).
+flag), 4 wave 0 (counts a time-out), 5 split-mode first chunk (no tile of
+its own: ends after publishing).
 
 Sparse-row segments (pair balancing, dispatch.cpp PreparePairs): a virtual
 entry x in [0, ntot) is the CSR entry x + (x < n1 ? b1 : b2m) (b2m = b2 - n1).
@@ -760,6 +761,9 @@ def _build(dt, wave_epi, last_block, stamps):
     body += step(dt, 0, zero_c=True)
     body.append("s_branch L_mid_%=")
     body.append("L_zero_%=:")
+    # a split-mode first chunk (flags bit 5) has no tile of its own: done
+    # once its partial is published
+    body += ["s_bitcmp1_b32 %[flags], 5", "s_cbranch_scc1 L_fin_%="]
     body += [f"v_accvgpr_write_b32 a{i}, 0" for i in range(256)]
     body.append("L_exit_%=:")
     if stamps:
@@ -793,6 +797,7 @@ def _build(dt, wave_epi, last_block, stamps):
     body += copy_out() if wave_epi else ["s_waitcnt lgkmcnt(0)"]
     if VARIANT["bar2"]:
         body.append("L_end_%=:")
+    body.append("L_fin_%=:")
     if stamps:
         body += ["s_memrealtime %[r2]", "s_waitcnt lgkmcnt(0)"]
     return body
