@@ -480,6 +480,8 @@ class PairProblem:
         self.anchor_shape = (dim, dim, int(round(dim * density)))
         self.bytes = 2 * (nz * 2 + 2 * dim * dim * 2) + nb * 8
         self.dtype_code = 0 if dtype == "f16" else 1
+        self.kernel = ("block_gemm_kernel (SDD, k-split 128x128 tile) + "
+                       "dsd4w_kernel (DDS NN, 4 waves)")
         self.desc = (f"SDD(x,w)->C then DDS(g,C) block=128 M=K=N={dim} "
                      f"density={density} {dtype} (MatmulEx metadata)")
 
@@ -603,7 +605,11 @@ class OpProblem:
                      f"density={dens} {args.dtype} "
                      f"({'MatmulEx' if args.api == 'ex' else 'Matmul'}"
                      f"{', device Transpose in every step' if meta_t and args.api == 'matmul' else ''})")
-        self.kernel = f"block_gemm_kernel<{args.dtype}, {op.upper()} {args.trans}>"
+        # (dispatch.cpp picks: the 4-wave dsd4w_kernel for every DSD / DDS
+        # transpose on one-tile-per-CU or split launches and the grouped
+        # SDD, block_gemm_kernel otherwise)
+        self.kernel = (f"{op.upper()} {args.trans} {args.dtype}: dsd4w_kernel where it "
+                       f"applies, else block_gemm_kernel")
 
     def launcher(self):
         import torch
