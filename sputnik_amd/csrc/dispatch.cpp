@@ -391,14 +391,14 @@ static int Dsd4wMode() {
   if (v < 0) {
     const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
     v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 6 ? 6 : v);
+    v = v < 0 ? 1 : (v > 7 ? 7 : v);
     g_dsd4w.store(v, std::memory_order_relaxed);
   }
   return v;
 }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2..6: wherever the kernel can run, whatever the density (tests, A/B), with
-// epilogue 0 / 1 / 2 / 3 / 4 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
+// 2..7: wherever the kernel can run, whatever the density (tests, A/B), with
+// epilogue 0 .. 5 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
 bool Dsd4wForced() { return Dsd4wMode() >= 2; }
 int Dsd4wEpi() {
   const int m = Dsd4wMode();
@@ -407,7 +407,7 @@ int Dsd4wEpi() {
 int SelectDsdKernel(int four_wave) {
   const int prev = Dsd4wMode();
   if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 6 ? 6 : four_wave, std::memory_order_relaxed);
+    g_dsd4w.store(four_wave > 7 ? 7 : four_wave, std::memory_order_relaxed);
   return prev;
 }
 
@@ -892,8 +892,16 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   const bool tall = UseTall(&p, stream);
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
-                   !ta, tb, false, tall))
-    return LaunchDsd4w(dtype, p, Dsd4wEpi(), tb && !ta, stream, ta && !tb, ta && tb);
+                   !ta, tb, false, tall)) {
+    // Default epilogue by density: below a mean of 12 blocks per block-row
+    // the copy-out interleaved with the staging (kEpi 5) is ahead (DSD NN
+    // 4096^3 A/B r04ae, two runs: 10% +1.5 / +1.2%, 30% +1.0 / +0.5%), at
+    // 50% behind (-0.6 / -0.3%).
+    int epi = Dsd4wEpi();
+    if (Dsd4wMode() == 1 && a.nonzeros / (kBlock * kBlock) < 12LL * p.num_rows)
+      epi = 5;
+    return LaunchDsd4w(dtype, p, epi, tb && !ta, stream, ta && !tb, ta && tb);
+  }
   return LaunchBlockGemm(dtype, false, !ta, tb, false, tall, p, stream);
 }
 

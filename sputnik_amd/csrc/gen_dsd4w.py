@@ -124,7 +124,9 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False, "tn": False, "ddstt": False}
+           "bar2": False, "tn": False, "ddstt": False, "il": False}
+# "il": the plain per-wave epilogue stores each 16-row batch as soon as it is
+# staged (on with "bar2"; alone: _W4).
 # DDS TT ("ddstt", with "ds"): B's rows (storage order) are the shared image
 # in double slots as in DSD; A stored [k][m] gives each wave a per-step [32 k]
 # [128 m] slice as DSD's B, read transposed into the B operand (%[vrt<m>]),
@@ -705,13 +707,14 @@ def poll():
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False):
-    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt)
+          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False):
+    VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt,
+                   il=il)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
         VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
-                       tn=False, ddstt=False)
+                       tn=False, ddstt=False, il=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -778,9 +781,9 @@ def _build(dt, wave_epi, last_block, stamps):
         # for the staging image
         body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
     body += ["s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc1 L_collect_%="]
-    if VARIANT["bar2"]:
-        # (with bar2: the plain epilogue stores each 16-row batch as soon as
-        # its 8 tiles are staged)
+    if VARIANT["bar2"] or VARIANT["il"]:
+        # (with bar2 / il: the plain epilogue stores each 16-row batch as
+        # soon as its 8 tiles are staged)
         body += epilogue_plain_interleaved(cvt)
         body.append("s_branch L_end_%=")
     else:
@@ -795,7 +798,7 @@ def _build(dt, wave_epi, last_block, stamps):
     body += epilogue_body(cvt, "nan", wave_epi)
     body += ["L_done_%=:"]
     body += copy_out() if wave_epi else ["s_waitcnt lgkmcnt(0)"]
-    if VARIANT["bar2"]:
+    if VARIANT["bar2"] or VARIANT["il"]:
         body.append("L_end_%=:")
     body.append("L_fin_%=:")
     if stamps:
@@ -842,6 +845,10 @@ def render():
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_DDS_TT \\")
         lines += [f'  "{ins}\\n" \\'
                   for ins in build(dt, True, dds=True, ds=True, ddstt=True)]
+        lines += ['  ""', ""]
+        # _W4: double slots with the interleaved plain epilogue (DSD)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W4 \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, ds=True, il=True)]
         lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
