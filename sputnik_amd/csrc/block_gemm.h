@@ -198,9 +198,6 @@ struct GemmParams {
   // Stored blocks of the sparse operand S (DSD: A's nonzeros / 128^2); the
   // 4-wave DSD kernel preloads an index list this short (dsd4w.hip).
   int s_blocks;
-  // Smallest pair hand-off (blocks) of the 4-wave kernel; 0: its default
-  // (dsd4w.hip; the 8-wave kernel uses SPUTNIK_MIN_HANDOFF).
-  int min_handoff;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

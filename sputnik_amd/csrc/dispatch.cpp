@@ -288,11 +288,6 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   if (p->num_tiles > slot->slots) return;
   if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
   p->pair = 1;
-  // 4-wave kernel: below a mean of 6 blocks per block-row a hand-off of 2
-  // blocks costs more (publish + collect) than it balances: 3 there (A/B
-  // r04af, separate libraries: DSD 4096^3 10% +3.5%; at 30% / 50% 3 was
-  // 0.4-0.5% behind 2, 1 behind everywhere).
-  p->min_handoff = blocks < 6LL * p->num_rows ? 3 : 2;
   p->pair_partials = slot->partials;
   p->pair_flags = slot->flags;
   p->pair_epoch = slot->epoch;
