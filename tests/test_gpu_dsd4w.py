@@ -571,3 +571,36 @@ def test_dds4w_tt_bit_identical_to_8wave(m, k, n, density, dtype):
             ref = O.gemm(av, True, blk, True, threads=H.oracle_threads())
             H.assert_close(c4[:, r * 128:(r + 1) * 128].float().cpu().numpy(), ref,
                            "f16" if dtype == "f16" else "bf16", f"dds4w TT col {r}")
+
+
+def test_dsd4w_index_preload_odd_count_last_entry():
+    """Regression: the index list is preloaded with 16-byte buffer loads
+    whose range check is per dword; with an odd number of entries the last
+    entry shares its dword with the end of the list. Block-rows of 3, 3,
+    ..., 2, 1 blocks (93 entries): the last row holds only entry 92 and runs
+    as a plain tile whose first k-block comes from the preload."""
+    R = 32
+    counts = [3] * 30 + [2, 1]
+    off = np.zeros(R + 1, np.int32)
+    np.cumsum(counts, out=off[1:])
+    rng = np.random.default_rng(4)
+    idx = np.concatenate([np.sort(rng.choice(np.arange(1, 32), c, replace=False))
+                          for c in counts]).astype(np.int16)
+    nb = int(off[-1])
+    assert nb % 2 == 1 and idx[-1] != 0
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    a = (torch.rand(nb * 16384, generator=g, device="cuda") * 2 - 1).half()
+    b = (torch.rand(4096 * 4096, generator=g, device="cuda") * 2 - 1).half()
+    A = sp.BlockMatrix(4096, 4096, 128, nb * 16384, a,
+                       torch.from_numpy(off).cuda(), torch.from_numpy(idx).cuda())
+    B = sp.Matrix(4096, 4096, b)
+    c4 = _run(A, B, 4096, 4096, "f16", 5)
+    c8 = _run(A, B, 4096, 4096, "f16", 0)
+    assert torch.equal(c4, c8)
+    av = a.float().cpu().numpy().reshape(-1, 128, 128)
+    bv = b.float().cpu().numpy().reshape(4096, 4096)
+    e = nb - 1
+    ref = O.gemm(av[e], False, bv[int(idx[e]) * 128:(int(idx[e]) + 1) * 128], False,
+                 threads=H.oracle_threads())
+    H.assert_close(c4[31 * 128:].float().cpu().numpy(), ref, "f16", "last block-row")
