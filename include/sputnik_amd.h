@@ -174,24 +174,44 @@ int sputnik_dsd_plan(const sputnik_block_matrix_t *a, int transpose_a,
  * launch to detect the (otherwise unobserved) event. Clears the counts.
  * Synchronizes the device. -1 on a HIP error. */
 int sputnik_pair_errors(void);
-/* Test knob: when on, pair producers never publish (forces the timeout). */
-void sputnik_debug_pair_fault(int on);
 /* Workspaces made for launches captured into graphs on the current device
  * (pair-balancing workspaces + persistent tile counters). A captured launch
- * gets one per (capture, capturing stream); it is freed once the captured
- * graph and every executable made from it are destroyed (the count drops at
- * the next eager launch or query). A graph must not be replayed
- * concurrently with a second instantiation of the same capture. Host-only
- * query. */
+ * gets one per (capture, capturing stream). Once the captured graph and
+ * every executable made from it are destroyed, its workspace is re-used by
+ * the next capture that needs one, and this call frees the ones still
+ * unused (the only place the library frees them: no free ever runs inside
+ * a launch). A graph must not be replayed concurrently with a second
+ * instantiation of the same capture. Host-only query. */
 int sputnik_capture_workspaces(void);
-/* DSD NN / DDS NN kernel choice (tests and same-process A/B): 1 = the
- * 4-wave hand-scheduled kernel where it applies and pays (the default;
- * environment SPUTNIK_AMD_DSD4W=0 turns it off), 2 / 3 / 4 / 5 = wherever it
- * applies, whatever the density, with its workgroup / per-wave / per-wave +
- * specialized-last-block / per-wave + double-slot k-contiguous image
- * variant (DDS: 3 for 2 and 4), 0 = the 8-wave kernel everywhere, -1 =
- * query only. Returns the previous choice. Process-wide. */
+
+/* ---- Test hooks and tuning knobs: UNSUPPORTED.
+ * For the library's own tests and same-process A/B experiments; a correct
+ * caller never needs them, names and ranges may change between versions,
+ * and every setting is process-wide. */
+/* Test hook: when on, pair producers never publish (forces the timeout).
+ * Same as sputnik_tuning_set("pair_fault", on). */
+void sputnik_debug_pair_fault(int on);
+/* Kernel choice for DSD / DDS (every transpose) and the grouped SDD: 1 =
+ * the 4-wave hand-scheduled kernel where it applies and pays (the default),
+ * 2..7 = wherever it applies, whatever the density, with the DSD NN variant
+ * kEpi = mode - 2 (0 workgroup epilogue, 1 per-wave, 2 per-wave +
+ * specialized last block, 3 double slots, 4 double slots + barrier every
+ * other step + interleaved copy-out, 5 double slots + interleaved copy-out;
+ * DDS NN runs kEpi 1 for modes 2-4 and kEpi 3 for 5-7, the grouped SDD the
+ * barrier-every-other-step variant for mode 6 and double slots otherwise,
+ * the transposed DSD / DDS launches the one variant they have), 0 = the
+ * 8-wave kernel everywhere, -1 = query only. Returns the previous choice.
+ * Same as the knob "dsd4w". */
 int sputnik_select_dsd_kernel(int four_wave);
+/* Tuning knobs, each initialised from its environment variable
+ * SPUTNIK_AMD_<NAME> (upper case) or its default: "pairs" (1), "pair_xcd2"
+ * (3), "split" (1), "split_min_bn" (128), "dsd4w" (1), "grouped_sdd" (1),
+ * "grouped_min_per_cu" (5), "tall" (1), "tall_persistent" (1), "dds_xcd2"
+ * (0), "sdd4w_max_ld" (16384), "pair_fault" (0). get returns the value,
+ * set the previous value; both return INT_MIN for an unknown name, set also
+ * for a value out of the knob's range (nothing changes then). */
+int sputnik_tuning_get(const char *name);
+int sputnik_tuning_set(const char *name, int value);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-5 parity session: the regular session (smoke, full GPU suite incl.
+# the topology fuzz and the full-output config tests, the driver's bench
+# command and its trace), then the new parity tests against
+# build/exp/preload_bug.so (scripts/build_preload_bug.sh: the f327921
+# index-preload bug on today's sources), which must FAIL.
+TAG=$1
+R=$GRAFT_REPO_ROOT
+bash $R/scripts/gpu_session.sh $TAG 1 - -; rc=$?
+[ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+OUT=$R/gpurun_out/$TAG
+cd $R
+echo "== bug_lib" | tee -a $OUT/steps.log
+SPUTNIK_AMD_LIB=$R/build/exp/preload_bug.so timeout -k 10 600 python -u -m pytest \
+  tests/test_gpu_dsd4w.py::test_dsd4w_index_preload_odd_count_last_entry \
+  tests/test_gpu_fuzz.py -q -p no:cacheprovider --timeout 120 --timeout-method thread \
+  -k "dsd or dds" --junitxml=$OUT/junit_bug.xml > $OUT/bug_lib.log 2>&1; rc2=$?
+echo "== bug_lib rc=$rc2 (1 = tests failed, as they must)" | tee -a $OUT/steps.log
+tail -5 $OUT/bug_lib.log
+[ $rc2 -eq 1 ] && exit $rc
+exit 3

@@ -117,6 +117,8 @@ _SIGNATURES = {
     "sputnik_debug_pair_fault": [ctypes.c_int],
     "sputnik_capture_workspaces": [],
     "sputnik_select_dsd_kernel": [ctypes.c_int],
+    "sputnik_tuning_get": [ctypes.c_char_p],
+    "sputnik_tuning_set": [ctypes.c_char_p, ctypes.c_int],
     "sputnik_dsd_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P],
 }
 _RESTYPES = {
@@ -440,6 +442,24 @@ def select_dsd_kernel(four_wave: int = -1) -> int:
     return int(lib().sputnik_select_dsd_kernel(int(four_wave)))
 
 
+TUNING_UNKNOWN = -(2 ** 31)
+
+
+def tuning(name: str, value: Optional[int] = None) -> int:
+    """UNSUPPORTED tuning knob (sputnik_tuning_get / sputnik_tuning_set,
+    include/sputnik_amd.h; tests and A/B experiments only): returns the
+    knob's value, or with `value` sets it and returns the previous one.
+    Raises KeyError for an unknown name or an out-of-range value."""
+    L = lib()
+    if value is None:
+        v = int(L.sputnik_tuning_get(name.encode()))
+    else:
+        v = int(L.sputnik_tuning_set(name.encode(), int(value)))
+    if v == TUNING_UNKNOWN:
+        raise KeyError(f"tuning knob {name!r} (value {value!r})")
+    return v
+
+
 def version() -> str:
     return lib().sputnik_version().decode()
 
@@ -454,7 +474,7 @@ __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
     "build_hash", "capture_workspaces", "pair_errors", "sdd_plan",
-    "select_dsd_kernel", "dsd_plan",
+    "select_dsd_kernel", "dsd_plan", "tuning",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",
     "FreeTransposeBuffers", "Matmul", "MatmulEx", "Matrix", "RowIndices",

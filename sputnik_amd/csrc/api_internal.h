@@ -62,12 +62,36 @@ int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
 int PairErrors();
 void SetPairFault(int on);
 int CaptureWorkspaces();
-// DSD NN: 4-wave kernel on (1) / off (0) / forced regardless of density
-// with epilogue 0, 1, 2 (2, 3, 4); -1 queries. Returns the previous.
+// DSD / DDS / grouped SDD: 4-wave kernel on (1) / off (0) / forced
+// regardless of density with kEpi = mode - 2 (modes 2-7, dsd4w.h
+// LaunchDsd4w); -1 queries. Returns the previous. (= knob "dsd4w")
 int SelectDsdKernel(int four_wave);
 bool Dsd4wEnabled();
 bool Dsd4wForced();
 int Dsd4wEpi();
+
+// Unsupported tuning knobs (dispatch.cpp kKnobs: name, environment
+// variable, default, range). Knob() reads one; TuningGet / TuningSet back
+// sputnik_tuning_get / sputnik_tuning_set (INT_MIN: unknown name or value
+// out of range).
+enum KnobId {
+  kKnobPairs,
+  kKnobPairXcd2,
+  kKnobSplit,
+  kKnobSplitMinBn,
+  kKnobDsd4w,
+  kKnobGroupedSdd,
+  kKnobGroupedMinPerCu,
+  kKnobTall,
+  kKnobTallPersistent,
+  kKnobDdsXcd2,
+  kKnobSdd4wMaxLd,
+  kKnobPairFault,
+  kNumKnobs
+};
+int Knob(KnobId k);
+int TuningGet(const char *name);
+int TuningSet(const char *name, int value);
 
 }  // namespace sputnik_amd
 

@@ -285,6 +285,12 @@ int sputnik_select_dsd_kernel(int four_wave) {
   return sputnik_amd::SelectDsdKernel(four_wave);
 }
 
+int sputnik_tuning_get(const char *name) { return sputnik_amd::TuningGet(name); }
+
+int sputnik_tuning_set(const char *name, int value) {
+  return sputnik_amd::TuningSet(name, value);
+}
+
 size_t sputnik_abi_block_matrix_size(void) { return sizeof(BlockMatrix); }
 
 size_t sputnik_abi_block_matrix_offset(int field) {

@@ -20,6 +20,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 
 #include "api_internal.h"
@@ -71,7 +72,8 @@ struct PairSlot {
   unsigned long long capture = 0;  // capture id (capture table only)
   // Capture table only: set (by a user-object destructor on HIP's callback
   // thread) once the captured graph and every executable made from it are
-  // destroyed; ReclaimCaptureSlots then frees the memory.
+  // destroyed; the slot is then re-tied to the next capture that needs one
+  // (PreparePairs / UseTall) or freed by sputnik_capture_workspaces().
   std::atomic<int> released{0};
   float *partials = nullptr;
   unsigned *flags = nullptr;  // [pairs] flags, the error word, [epoch, count]
@@ -84,7 +86,70 @@ constexpr int kMaxCaptureSlots = 64;
 static PairSlot g_pairs[kMaxPairSlots];
 static PairSlot g_capture_pairs[kMaxCaptureSlots];
 static std::mutex g_pairs_mu;
-static int g_pair_fault = 0;  // test knob (sputnik_debug_pair_fault)
+
+// ---- tuning knobs ---------------------------------------------------------
+// Unsupported switches for same-process A/B experiments and tests (documented
+// as such in include/sputnik_amd.h and INTEGRATION.md §6). Each starts from
+// its environment variable, else its default, on first use; the C-ABI's
+// sputnik_tuning_set() changes it at run time (process-wide). Defaults are
+// the shipped configuration; nothing in a correct caller needs them.
+struct KnobDef {
+  const char *name;
+  const char *env;
+  int def, lo, hi;
+};
+static const KnobDef kKnobs[kNumKnobs] = {
+    {"pairs", "SPUTNIK_AMD_PAIRS", 1, 0, 1},
+    {"pair_xcd2", "SPUTNIK_AMD_PAIR_XCD2", 3, 0, 3},
+    {"split", "SPUTNIK_AMD_SPLIT", 1, 0, 1},
+    {"split_min_bn", "SPUTNIK_AMD_SPLIT_MIN_BN", 128, 0, 1 << 20},
+    {"dsd4w", "SPUTNIK_AMD_DSD4W", 1, 0, 7},
+    {"grouped_sdd", "SPUTNIK_AMD_GROUPED_SDD", 1, 0, 1},
+    {"grouped_min_per_cu", "SPUTNIK_AMD_GROUPED_MIN_PER_CU", 5, 0, 1 << 20},
+    {"tall", "SPUTNIK_AMD_TALL", 1, 0, 2},
+    {"tall_persistent", "SPUTNIK_AMD_TALL_PERSISTENT", 1, 0, 1},
+    {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 0, 0, 3},
+    {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 16384, 0, 1 << 30},
+    {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
+};
+constexpr int kKnobUnset = -0x7fffffff - 1;
+static std::atomic<int> g_knobs[kNumKnobs];
+static std::once_flag g_knobs_once;
+
+static void InitKnobs() {
+  std::call_once(g_knobs_once, [] {
+    for (int i = 0; i < kNumKnobs; ++i) {
+      const char *e = std::getenv(kKnobs[i].env);
+      int v = e != nullptr ? std::atoi(e) : kKnobs[i].def;
+      v = v < kKnobs[i].lo ? kKnobs[i].lo : v > kKnobs[i].hi ? kKnobs[i].hi : v;
+      g_knobs[i].store(v, std::memory_order_relaxed);
+    }
+  });
+}
+
+int Knob(KnobId k) {
+  InitKnobs();
+  return g_knobs[k].load(std::memory_order_relaxed);
+}
+
+static int KnobIndex(const char *name) {
+  if (name == nullptr) return -1;
+  for (int i = 0; i < kNumKnobs; ++i)
+    if (std::strcmp(name, kKnobs[i].name) == 0) return i;
+  return -1;
+}
+
+int TuningGet(const char *name) {
+  const int i = KnobIndex(name);
+  return i < 0 ? kKnobUnset : Knob(static_cast<KnobId>(i));
+}
+
+int TuningSet(const char *name, int value) {
+  const int i = KnobIndex(name);
+  if (i < 0 || value < kKnobs[i].lo || value > kKnobs[i].hi) return kKnobUnset;
+  InitKnobs();
+  return g_knobs[i].exchange(value, std::memory_order_relaxed);
+}
 
 // Tile counter pair of persistent tall launches, per (device, stream): the
 // kernel resets it to zero at the end of every launch (GemmParams::
@@ -203,11 +268,7 @@ static bool PairsEnabled() {
 #ifdef SPUTNIK_NO_PAIRS
   return false;
 #endif
-  static const int enabled = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_PAIRS");
-    return e ? std::atoi(e) : 1;
-  }();
-  return enabled != 0;
+  return Knob(kKnobPairs) != 0;
 }
 
 // Fills the pair fields of p when pair balancing applies: a staggered
@@ -222,7 +283,10 @@ static bool PairsEnabled() {
 #ifndef SPUTNIK_PAIR_XCD2_DEFAULT
 #define SPUTNIK_PAIR_XCD2_DEFAULT 3
 #endif
-static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
+// dry: decide only (DsdPlan): no workspace is allocated, re-tied or
+// advanced, and the pointers stay null.
+static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream,
+                         bool dry = false) {
   p->pair = 0;
   if (!CfgSparse::kStagger || CfgSparse::kWGs != 1)
     return;
@@ -235,7 +299,6 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
-  if (!capturing) ReclaimCaptureSlots();
   PairSlot *table = capturing ? g_capture_pairs : g_pairs;
   const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   PairSlot *slot = nullptr;
@@ -247,6 +310,31 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
       break;
     }
   }
+  // A capture-table slot whose graph is gone is re-tied to the graph being
+  // captured, memory and device epoch word as they are: the word only ever
+  // grows, so the flags the old graph left can never match a new launch, and
+  // its arrival count is back at zero (the last arriver of every launch
+  // resets it). No HIP free on this path (frees happen in
+  // sputnik_capture_workspaces()).
+  if (slot == nullptr && capturing) {
+    for (int i = 0; i < n_table; ++i) {
+      PairSlot &s = table[i];
+      if (s.partials != nullptr && s.device == dev &&
+          s.released.load(std::memory_order_acquire) != 0) {
+        if (dry) {
+          slot = &s;
+          break;
+        }
+        s.stream = stream;
+        s.capture = capture;
+        s.released.store(0, std::memory_order_relaxed);
+        (void)TieToCapturedGraph(stream, &s.released);
+        slot = &s;
+        break;
+      }
+    }
+  }
+  PairSlot dry_slot;
   if (slot == nullptr) {
     for (int i = 0; i < n_table; ++i)
       if (table[i].partials == nullptr) {
@@ -254,12 +342,17 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
         break;
       }
     if (slot == nullptr) {
-      WarnSlotsFull(capturing ? 2 : 0);
+      if (!dry) WarnSlotsFull(capturing ? 2 : 0);
       return;
     }
     const int cus = DeviceCUs(dev);
     if (cus <= 0) return;
     const int slots = cus * CfgSparse::kWGs;
+    if (dry) {  // the workspace a launch would allocate
+      dry_slot.slots = slots;
+      dry_slot.pairs = slots / 2;
+      slot = &dry_slot;
+    } else {
     // Partial slots: slots / 2 pairs, or one per tile in split mode (at most
     // slots / 2 tiles). 128 x 256 KiB = 32 MiB per workspace on MI355X.
     const int pairs = slots / 2;
@@ -284,16 +377,19 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     slot->slots = slots;
     slot->released.store(0, std::memory_order_relaxed);
     if (capturing) (void)TieToCapturedGraph(stream, &slot->released);
+    }
   }
   if (p->num_tiles > slot->slots) return;
-  if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
   p->pair = 1;
-  p->pair_partials = slot->partials;
-  p->pair_flags = slot->flags;
-  p->pair_epoch = slot->epoch;
-  p->pair_error = slot->flags + slot->pairs;
-  p->pair_sync = capturing ? slot->flags + slot->pairs + 1 : nullptr;
-  p->pair_fault = g_pair_fault;
+  if (!dry) {
+    if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
+    p->pair_partials = slot->partials;
+    p->pair_flags = slot->flags;
+    p->pair_epoch = slot->epoch;
+    p->pair_error = slot->flags + slot->pairs;
+    p->pair_sync = capturing ? slot->flags + slot->pairs + 1 : nullptr;
+  }
+  p->pair_fault = Knob(kKnobPairFault);
   // Two panels x half the pairs per XCD (GemmParams::pair_xcd2) from a mean
   // of 8 blocks per row: DSD 4096^3 A/B (r02m) 30% / 50% / 90% +1.2 / +2.7
   // / +2.8%, 10% -4.4%. SPUTNIK_AMD_PAIR_XCD2=0 turns it off. Mode 3 (the
@@ -304,10 +400,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   // 1 had put the critical pairs exactly there (4-wave A/B, separate
   // processes, 30/50/90%: +1.0/+2.1/+1.4%, 10% +0.5%). Mode 2 interleaves
   // the pairs (r04d: +0.5% at 50%).
-  static const int xcd2 = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_PAIR_XCD2");
-    return e != nullptr ? std::atoi(e) : SPUTNIK_PAIR_XCD2_DEFAULT;
-  }();
+  const int xcd2 = Knob(kKnobPairXcd2);
   p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? xcd2 : 0;
   // Split mode (GemmParams::pair_split) when the tiles fill at most half of
   // the workgroup slots (e.g. 512-2048-row panels of a strong-scaled 4096^2,
@@ -315,10 +408,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
   // workgroups per tile. SPUTNIK_AMD_SPLIT=0 turns it off. (r03b, DSD
   // K=N=4096 50%: M=512 45.2 -> 34.6 us, 1024 47.6 -> 38.4, 2048 48.8 ->
   // 45.2; 4 or 8 workgroups per tile were slower.)
-  static const int split_on = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_SPLIT");
-    return e != nullptr ? std::atoi(e) : 1;
-  }();
+  const int split_on = Knob(kKnobSplit);
   // Tile width: the narrowest of 512 / 256 / 128 columns whose tiles (two
   // workgroups each) still fit the slots, so a panel of few block-rows
   // fills the CUs (r03: M = 512 on 128-column tiles, M = 1024 on 256).
@@ -336,11 +426,8 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream) {
     // Tuning floor of the tile width: 512 keeps the wide tile. Only the
     // three instantiated widths are valid (Launch has split kernels for 128,
     // 256 and 512 columns); anything else is rounded up to the next one.
-    static const int max_narrow = [] {
-      const char *e = std::getenv("SPUTNIK_AMD_SPLIT_MIN_BN");
-      const int v = e != nullptr ? std::atoi(e) : 128;
-      return v <= 128 ? 128 : v <= 256 ? 256 : CfgSparse::kBN;
-    }();
+    const int mbn = Knob(kKnobSplitMinBn);
+    const int max_narrow = mbn <= 128 ? 128 : mbn <= 256 ? 256 : CfgSparse::kBN;
     if (bn < max_narrow) bn = max_narrow;
     p->split_bn = bn;
     p->num_jtiles = (p->j_limit + bn - 1) / bn;
@@ -380,22 +467,12 @@ int PairErrors() {
   return total;
 }
 
-void SetPairFault(int on) { g_pair_fault = on != 0; }
+void SetPairFault(int on) { (void)TuningSet("pair_fault", on != 0 ? 1 : 0); }
 
 // DSD NN kernel selection: the 4-wave hand-scheduled kernel (dsd4w.hip) where
-// it applies, else the 8-wave block_gemm_kernel. SPUTNIK_AMD_DSD4W=0 (or
-// sputnik_select_dsd_kernel(0), tests and A/B) keeps the 8-wave kernel.
-static std::atomic<int> g_dsd4w{-1};
-static int Dsd4wMode() {
-  int v = g_dsd4w.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char *e = std::getenv("SPUTNIK_AMD_DSD4W");
-    v = e != nullptr ? std::atoi(e) : 1;
-    v = v < 0 ? 1 : (v > 7 ? 7 : v);
-    g_dsd4w.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
+// it applies, else the 8-wave block_gemm_kernel. Knob "dsd4w" 0 (tests and
+// A/B) keeps the 8-wave kernel.
+static int Dsd4wMode() { return Knob(kKnobDsd4w); }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
 // 2..7: wherever the kernel can run, whatever the density (tests, A/B), with
 // epilogue 0 .. 5 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
@@ -405,10 +482,8 @@ int Dsd4wEpi() {
   return m >= 2 ? m - 2 : kDsd4wDefaultEpi;
 }
 int SelectDsdKernel(int four_wave) {
-  const int prev = Dsd4wMode();
-  if (four_wave >= 0)
-    g_dsd4w.store(four_wave > 7 ? 7 : four_wave, std::memory_order_relaxed);
-  return prev;
+  if (four_wave < 0) return Dsd4wMode();
+  return TuningSet("dsd4w", four_wave > 7 ? 7 : four_wave);
 }
 
 static void ReclaimCaptureSlots() {
@@ -752,11 +827,7 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
 #ifdef SPUTNIK_NO_GROUPED_SDD
   return false;
 #endif
-  static const int disabled = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_GROUPED_SDD");
-    return e != nullptr && std::atoi(e) == 0;
-  }();
-  if (disabled || c.offsets == nullptr) return false;
+  if (Knob(kKnobGroupedSdd) == 0 || c.offsets == nullptr) return false;
   constexpr int kGrp = CfgSddGrouped::kBN / kBlock;
   const int blocks = p->num_tiles;
   int dev = 0;
@@ -766,15 +837,11 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   // From 5 blocks per CU the grouped tile is faster (SDD 8192^2 x 8192,
   // scripts/exp_grp.sh, r02: 4 per CU k-split 318 vs grouped 362 us; 5 per
   // CU 399 vs 365; 6 per CU 491 vs 387; 8 per CU 652 vs 570).
-  // SPUTNIK_AMD_GROUPED_MIN_PER_CU moves the switch (tuning only; never
-  // below kGrp, so a grouped grid still fills every CU).
-  constexpr int kGroupedMinPerCu = 5;
-  static_assert(kGroupedMinPerCu >= kGrp, "a grouped grid fills every CU");
-  static const int min_per_cu = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_GROUPED_MIN_PER_CU");
-    const int v = e != nullptr ? std::atoi(e) : kGroupedMinPerCu;
-    return v < kGrp ? kGrp : v;
-  }();
+  // Knob "grouped_min_per_cu" (default 5) moves the switch (tuning only;
+  // never below kGrp, so a grouped grid still fills every CU).
+  static_assert(5 >= kGrp, "a grouped grid fills every CU");
+  const int min_per_cu = Knob(kKnobGroupedMinPerCu) < kGrp ? kGrp
+                                                             : Knob(kKnobGroupedMinPerCu);
   if (blocks < min_per_cu * cus || p->num_rows > kMaxGroupRows)
     return false;
   // D lane offsets: k-contiguous D gathers whole rows (n * ldb); otherwise
@@ -790,15 +857,10 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
 // Tall sparse operands (more block-rows than the in-kernel row ranking
 // handles, so no LPT order and no pair balancing) have many more tiles than
 // CUs: they run on CfgTall, two workgroups per CU.
-bool UseTall(GemmParams *p, hipStream_t stream) {
-  // SPUTNIK_AMD_TALL: 0 never, 2 always (experiments), unset: tall only.
-  static const int mode = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_TALL");
-#ifndef SPUTNIK_TALL_MODE
-#define SPUTNIK_TALL_MODE 1
-#endif
-    return e != nullptr ? std::atoi(e) : SPUTNIK_TALL_MODE;
-  }();
+// dry: decide only (DsdPlan), no counter allocated.
+bool UseTall(GemmParams *p, hipStream_t stream, bool dry = false) {
+  // knob "tall": 0 never, 2 always (experiments), 1 (default): tall only.
+  const int mode = Knob(kKnobTall);
   if (mode == 0) return false;
   if (mode == 2) {
     // Forced tall (experiments): drop every pair-launch setting PreparePairs
@@ -818,10 +880,7 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   // ~20% of the slots idle between a workgroup's end and the next dispatch
   // (r02 timeline: 400-460 of 512 resident); a static tile stride instead
   // loses more to imbalance (403 vs 337 us, config 5).
-  static const int persistent = [] {
-    const char *e = std::getenv("SPUTNIK_AMD_TALL_PERSISTENT");
-    return e != nullptr ? std::atoi(e) : 1;
-  }();
+  const int persistent = Knob(kKnobTallPersistent);
   int dev = 0;
   const int cus = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
   const int slots = cus * CfgTall::kWGs;
@@ -833,7 +892,6 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
   const int capturing = CaptureState(stream, &capture);
   if (capturing < 0) return true;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
-  if (!capturing) ReclaimCaptureSlots();
   CounterSlot *table = capturing ? g_capture_counters : g_counters;
   const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
   CounterSlot *slot = nullptr;
@@ -845,6 +903,24 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
       break;
     }
   }
+  // (a released capture slot is re-tied as in PreparePairs: the kernel left
+  // its counter pair at zero)
+  if (slot == nullptr && capturing) {
+    for (int i = 0; i < n_table; ++i) {
+      CounterSlot &c = table[i];
+      if (c.counter != nullptr && c.device == dev &&
+          c.released.load(std::memory_order_acquire) != 0) {
+        slot = &c;
+        if (!dry) {
+          c.stream = stream;
+          c.capture = capture;
+          c.released.store(0, std::memory_order_relaxed);
+          (void)TieToCapturedGraph(stream, &c.released);
+        }
+        break;
+      }
+    }
+  }
   if (slot == nullptr) {
     for (int i = 0; i < n_table; ++i)
       if (table[i].counter == nullptr) {
@@ -852,7 +928,12 @@ bool UseTall(GemmParams *p, hipStream_t stream) {
         break;
       }
     if (slot == nullptr) {
-      WarnSlotsFull(capturing ? 3 : 1);
+      if (!dry) WarnSlotsFull(capturing ? 3 : 1);
+      return true;
+    }
+    if (dry) {  // the counter a launch would allocate
+      p->grid = slots;
+      p->persistent = 1;
       return true;
     }
     void *ctr = nullptr;
@@ -924,11 +1005,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
       Dds4wApplies(p, Dsd4wForced() ? (1LL << 40) : b.nonzeros / (kBlock * kBlock),
                    tb, !ta, true, tall)) {
     // (the two-panel pair placement: DSD-measured; DDS experiment knob)
-    static const int dds_xcd2 = [] {
-      const char *e = std::getenv("SPUTNIK_AMD_DDS_XCD2");
-      return e != nullptr ? std::atoi(e) : 0;
-    }();
-    if (p.pair_xcd2 != 0) p.pair_xcd2 = dds_xcd2;
+    if (p.pair_xcd2 != 0) p.pair_xcd2 = Knob(kKnobDdsXcd2);
     return LaunchDds4w(dtype, p, Dsd4wEpi(), tb && !ta, stream, ta && !tb, ta && tb);
   }
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
@@ -1222,9 +1299,9 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
 
 // Which kernel RunDsd would launch for this problem on `stream` (no
 // launch): 0 the 8-wave 128 x 512 tile, 1 the 4-wave hand-scheduled kernel
-// (dsd4w.hip), 2 the tall configuration, 3 split mode, -1 rejected. Makes
-// the same workspace decisions a launch would (pair workspace, tile
-// counter), so it may allocate them.
+// (dsd4w.hip), 2 the tall configuration, 3 split mode, -1 rejected. Read-only:
+// it makes the workspace decisions a launch would make without allocating,
+// re-tying or advancing any workspace (safe during a capture).
 int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
             hipStream_t stream) {
   if (!a || !b || !c) return -1;
@@ -1234,8 +1311,8 @@ int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
   if (PrepareDsd(am, ta, *static_cast<const Matrix *>(b), tb,
                  *static_cast<const Matrix *>(c), &p, &needs_meta) != Status::kOk)
     return -1;
-  PreparePairs(&p, am.nonzeros / (kBlock * kBlock), stream);
-  const bool tall = UseTall(&p, stream);
+  PreparePairs(&p, am.nonzeros / (kBlock * kBlock), stream, /*dry=*/true);
+  const bool tall = UseTall(&p, stream, /*dry=*/true);
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : am.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall))

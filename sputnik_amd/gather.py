@@ -130,6 +130,9 @@ def gather_col_panels(c_panel, panels: Sequence[Tuple[int, int]], group=None,
     ``panels[r] = (c0, c1)``: rank r computed block-columns [c0, c1) of C as
     its ``c_panel`` [M, (c1 - c0) * 128] (``shard_cols_by_nnz``). The pieces
     travel as they are (each contiguous [M][w_r]) and land in their columns.
+    A caller's ``out`` must be a contiguous [M, N] tensor of c_panel's dtype
+    and device. Peak memory is twice the result: the pieces arrive in one
+    flat [M * N] staging tensor before they are placed in their columns.
     """
     import torch
     _check_cover(panels)
@@ -137,9 +140,15 @@ def gather_col_panels(c_panel, panels: Sequence[Tuple[int, int]], group=None,
     world = dist.get_world_size(group)
     widths = [(c1 - c0) * BLOCK for c0, c1 in panels]
     m = c_panel.shape[0]
+    n = sum(widths)
+    if out is not None and (tuple(out.shape) != (m, n) or not out.is_contiguous()
+                            or out.dtype != c_panel.dtype
+                            or out.device != c_panel.device):
+        raise ValueError(f"out must be a contiguous {(m, n)} {c_panel.dtype} tensor "
+                         f"on {c_panel.device}, got {tuple(out.shape)} {out.dtype} "
+                         f"on {out.device}")
     flat = allgather_concat(c_panel.contiguous().reshape(-1), [m * w for w in widths],
                             group=group, method=method)
-    n = sum(widths)
     if out is None:
         out = torch.empty((m, n), dtype=c_panel.dtype, device=c_panel.device)
     pos = 0

@@ -158,3 +158,37 @@ def test_dsd4w_asm_matches_generator():
     spec.loader.exec_module(mod)
     with open(os.path.join(root, "sputnik_amd", "csrc", "dsd4w_asm.inc")) as f:
         assert f.read() == mod.render()
+
+
+def test_tuning_knobs_host_only():
+    """The unsupported tuning knobs (sputnik_tuning_get / _set, dispatch.cpp
+    kKnobs): defaults, set returns the previous value, range and name checks
+    change nothing, select_dsd_kernel is the "dsd4w" knob."""
+    import os as _os
+    defaults = {"pairs": 1, "pair_xcd2": 3, "split": 1, "split_min_bn": 128,
+                "dsd4w": 1, "grouped_sdd": 1, "grouped_min_per_cu": 5,
+                "tall": 1, "tall_persistent": 1, "dds_xcd2": 0,
+                "sdd4w_max_ld": 16384, "pair_fault": 0}
+    for name, v in defaults.items():
+        if "SPUTNIK_AMD_" + name.upper() not in _os.environ:
+            assert sp.tuning(name) == v, name
+    prev = sp.tuning("pairs", 0)
+    try:
+        assert sp.tuning("pairs") == 0
+        with pytest.raises(KeyError):
+            sp.tuning("pairs", 7)          # out of range: unchanged
+        assert sp.tuning("pairs") == 0
+    finally:
+        assert sp.tuning("pairs", prev) == 0
+    with pytest.raises(KeyError):
+        sp.tuning("no_such_knob")
+    prev = sp.select_dsd_kernel(5)
+    try:
+        assert sp.tuning("dsd4w") == 5
+    finally:
+        sp.select_dsd_kernel(prev)
+    L = sp.lib()
+    L.sputnik_debug_pair_fault(1)
+    assert sp.tuning("pair_fault") == 1
+    L.sputnik_debug_pair_fault(0)
+    assert sp.tuning("pair_fault") == 0

@@ -8,9 +8,10 @@ hide them:
             d_ff 14336, bf16 (SDD x.w1 at the expert blocks, DSD h.w2)
   config 5  DSD M=131072 K=N=4096 2%, and its row-panel split
 
-Full-size launches; the CPU oracle (oracle/) checks sampled block-rows /
-blocks, and size-independent properties (a row-sum checksum, exact zeros of
-empty rows, bit-identical sharded results) cover the rest. Tolerance as
+Full-size launches. Configs 2 and 3: every output element against the CPU
+oracle (oracle/). Configs 4 and 5: sampled block-rows / blocks, and
+size-independent properties (exact zeros of empty rows, bit-identical
+sharded results) cover the rest. Tolerance as
 tests/helpers.py (1e-2 relative fp16, 2e-2 bf16). Config 1 is the host
 reference alone (tests/test_oracle.py, bench.py's config-1 line).
 """
@@ -38,10 +39,11 @@ def _sync():
 
 
 @pytest.mark.parametrize("density", [0.1, 0.3, 0.5, 0.9])
-def test_dsd_baseline_config_sampled(density):
-    """BASELINE config 2 (M=K=N=4096) at its four densities: full GPU result,
-    oracle on 3 sampled block-rows (first, middle, last) + row-sum checksum
-    over all rows (linearity: C·1 = A·(B·1))."""
+def test_dsd_baseline_config_full(density):
+    """BASELINE config 2 (M=K=N=4096) at its four densities: EVERY output
+    element against the oracle (all 32 block-rows; the 16-thread oracle
+    with the zero-block skip takes ~2-16 s per density), plus a row-sum
+    checksum (linearity: C.1 = A.(B.1)) and the pair error count."""
     rng = np.random.default_rng(7)
     nz = mu.nonzeros_for_density(4096, 4096, density)
     A = H.HostSparse(4096, 4096, nz, rng)
@@ -49,13 +51,14 @@ def test_dsd_baseline_config_sampled(density):
     C, c_t = H.empty_dense(4096, 4096)
     sp.Matmul(A.matrix, False, B.matrix, False, C)
     _sync()
+    assert sp.pair_errors() == 0
     gpu = c_t.float().cpu().numpy()
     dense_a = A.dense()
-    for r in (0, 15, 31):
+    ref = O.gemm(dense_a, False, B.values, False, a_mask=A.mask(),
+                 threads=H.oracle_threads())
+    for r in range(32):
         rows = slice(r * 128, (r + 1) * 128)
-        ref = O.gemm(dense_a[rows], False, B.values, False,
-                     a_mask=A.mask()[r:r + 1], threads=H.oracle_threads())
-        H.assert_close(gpu[rows], ref, "f16", f"row-block {r}")
+        H.assert_close(gpu[rows], ref[rows], "f16", f"row-block {r}")
     ones = B.values.astype(np.float64).sum(axis=1)
     checksum = dense_a.astype(np.float64) @ ones
     got = gpu.astype(np.float64).sum(axis=1)
@@ -63,8 +66,10 @@ def test_dsd_baseline_config_sampled(density):
     assert np.abs(got - checksum).max() <= 2e-2 * scale + 1e-2 * np.abs(checksum).max()
 
 
-def test_sdd_dds_pair_config3():
-    """BASELINE config 3 (MegaBlocks fwd/bwd pair at 4096^3, 20%), sampled."""
+def test_sdd_dds_pair_config3_full():
+    """BASELINE config 3 (MegaBlocks fwd/bwd pair at 4096^3, 20%): every one
+    of the 205 SDD blocks and every element of the DDS output against the
+    oracle (the DDS on the SDD output as produced, rounded to fp16)."""
     rng = np.random.default_rng(11)
     nz = mu.nonzeros_for_density(4096, 4096, 0.2)
     x = H.HostDense(4096, 4096, rng)
@@ -78,21 +83,22 @@ def test_sdd_dds_pair_config3():
     out, out_t = H.empty_dense(4096, 4096)
     sp.Matmul(g.matrix, False, Cs.matrix, False, out)            # DDS
     _sync()
+    assert sp.pair_errors() == 0
     blocks = Cs.dev_values.float().cpu().numpy()
     rows = np.repeat(np.arange(32), np.diff(Cs.offsets))
-    for b in (0, len(rows) // 2, len(rows) - 1):
+    ref = O.gemm(x.values, False, w.values, False, out_mask=Cs.mask(),
+                 threads=H.oracle_threads())
+    for b in range(len(rows)):
         r, c = rows[b], Cs.indices[b]
-        ref = O.gemm(x.values[r * 128:(r + 1) * 128], False,
-                     w.values[:, c * 128:(c + 1) * 128], False)
-        H.assert_close(blocks[b], ref, "f16", f"sdd block {b}")
-    # DDS against the oracle on the SDD output as produced (rounded to fp16).
+        H.assert_close(blocks[b], ref[r * 128:(r + 1) * 128, c * 128:(c + 1) * 128],
+                       "f16", f"sdd block {b}")
     sdd_dense = mu.to_dense(4096, 4096, Cs.offsets, Cs.indices, blocks)
-    for r in (0, 17, 31):
-        ref = O.gemm(g.values[r * 128:(r + 1) * 128], False, sdd_dense, False,
-                     b_mask=Cs.mask(), threads=H.oracle_threads())
-        H.assert_close(out_t[r * 128:(r + 1) * 128].float().cpu().numpy(),
-                       ref, "f16", f"dds row-block {r}")
-
+    ref = O.gemm(g.values, False, sdd_dense, False, b_mask=Cs.mask(),
+                 threads=H.oracle_threads())
+    got = out_t.float().cpu().numpy()
+    for r in range(32):
+        H.assert_close(got[r * 128:(r + 1) * 128], ref[r * 128:(r + 1) * 128],
+                       "f16", f"dds row-block {r}")
 
 
 def test_moe_config4_bf16_sampled():

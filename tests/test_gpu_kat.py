@@ -538,6 +538,69 @@ def test_graph_capture_workspace_freed_with_graph():
     assert sp.pair_errors() == 0
 
 
+def test_graph_capture_reuses_released_workspace():
+    """Repeated capture / replay / destroy with no eager launch and no
+    sputnik_capture_workspaces() call in between: each new
+    capture re-ties the released workspace of the destroyed graph instead of
+    allocating another 32 MiB (device memory stays flat), replays stay
+    bit-exact, and sputnik_capture_workspaces() finally frees it."""
+    import time
+    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
+                                    "f16", seed=19)
+    torch.cuda.synchronize()
+    base = sp.capture_workspaces()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    free = []
+    for rep in range(6):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            sp.MatmulEx(A.m, False, Bd.m, False, C)
+        got.fill_(float("nan"))
+        g.replay()
+        _equal(got, want, f"replay {rep}")
+        torch.cuda.synchronize()
+        g.reset()
+        del g
+        torch.cuda.synchronize()
+        time.sleep(0.1)  # the release runs on HIP's callback thread
+        free.append(torch.cuda.mem_get_info()[0])
+    drop = free[1] - free[-1]
+    assert drop < 48 << 20, f"device memory fell by {drop >> 20} MiB over 4 captures"
+    n = sp.capture_workspaces()
+    for _ in range(50):
+        if n == base:
+            break
+        time.sleep(0.02)
+        n = sp.capture_workspaces()
+    assert n == base
+    assert sp.pair_errors() == 0
+
+
+def test_dsd_plan_is_read_only_under_capture():
+    """sputnik_dsd_plan decides without allocating: called while
+    a stream is being captured it creates no capture workspace, and it
+    reports the same plan as outside the capture."""
+    got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
+                                    "f16", seed=21)
+    torch.cuda.synchronize()
+    base = sp.capture_workspaces()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    plan_eager = sp.dsd_plan(A.m, False, Bd.m, False, C, stream=s.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        plan_cap = sp.dsd_plan(A.m, False, Bd.m, False, C, stream=s.cuda_stream)
+        assert sp.capture_workspaces() == base
+        sp.MatmulEx(A.m, False, Bd.m, False, C)
+    assert plan_cap == plan_eager == 1
+    assert sp.capture_workspaces() == base + 1
+    got.fill_(float("nan"))
+    g.replay()
+    _equal(got, want, "replay")
+    del g
+
+
 def test_graph_capture_split_and_dds():
     """Split mode (a 512-row DSD panel) and a pair-balanced DDS captured in
     one graph: two launches share the capture's workspace one after the

@@ -337,6 +337,19 @@ def _worker_gather(rank, world, port, out_path, method):
                     False, b_mask=mu.block_mask(q_off, q_idx, c1 - c0))
     dds = sp.gather_col_panels(torch.from_numpy(np.ascontiguousarray(cp)), cpan,
                                method=method)
+    # a caller's out of the wrong shape / dtype is refused before any
+    # collective (on every rank alike, so nothing hangs)
+    refused = 0
+    for bad in (torch.empty((M, 8)), torch.empty((M, NB * 128), dtype=torch.float64)):
+        try:
+            sp.gather_col_panels(torch.from_numpy(np.ascontiguousarray(cp)), cpan,
+                                 out=bad, method=method)
+        except ValueError:
+            refused += 1
+    outp = torch.empty((M, NB * 128))
+    dds2 = sp.gather_col_panels(torch.from_numpy(np.ascontiguousarray(cp)), cpan,
+                                out=outp, method=method)
+    assert dds2 is outp and torch.equal(dds2, dds)
     # SDD block runs (values stand in for computed blocks: the gather is what
     # is under test)
     runs = mu.shard_blocks(len(idx2), world)
@@ -344,7 +357,8 @@ def _worker_gather(rank, world, port, out_path, method):
     sdd = sp.gather_block_runs(torch.from_numpy(vals2[b0:b1].reshape(-1)), runs,
                                method=method)
     if rank == 0:
-        np.savez(out_path, dsd=dsd.numpy(), dds=dds.numpy(), sdd=sdd.numpy())
+        np.savez(out_path, dsd=dsd.numpy(), dds=dds.numpy(), sdd=sdd.numpy(),
+                 refused=refused)
     dist.destroy_process_group()
 
 
@@ -363,6 +377,7 @@ def test_gather_panels_match_unsharded(tmp_path, world, method):
     assert np.array_equal(got["dds"], O.gemm(
         a, False, mu.to_dense(KB * 128, NB * 128, off2, idx2, vals2), False))
     assert np.array_equal(got["sdd"], vals2)
+    assert int(got["refused"]) == 2
 
 
 def test_gather_checks_cover():
