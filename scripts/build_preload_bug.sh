@@ -1,14 +1,14 @@
 #!/bin/bash
-# Builds build/exp/preload_bug.so: the library of this tree with ONLY the
+# Builds build/bug/preload_bug.so: the library of this tree with ONLY the
 # 4-wave index-preload fix of fd7563c undone (num_records = the exact byte
 # size of the index list, so with an odd entry count the last entry reads 0;
 # the ADVICE r04 range guard in kblock_of removed too). It reproduces the bug
 # the f327921 library shipped with, on today's sources, so that the parity
 # tests (tests/test_gpu_fuzz.py, test_gpu_configs.py) can be shown to catch
-# it: SPUTNIK_AMD_LIB=build/exp/preload_bug.so python -m pytest ...
+# it: SPUTNIK_AMD_LIB=build/bug/preload_bug.so python -m pytest ...
 set -e
 ROOT=$(cd $(dirname $0)/.. && pwd)
-D=$ROOT/build/exp/preload_bug
+D=$ROOT/build/bug/preload_bug
 rm -rf $D && mkdir -p $D/csrc
 cp $ROOT/sputnik_amd/csrc/*.hip $ROOT/sputnik_amd/csrc/*.cpp $ROOT/sputnik_amd/csrc/*.h $ROOT/sputnik_amd/csrc/*.inc $D/csrc/
 sed -i 's/(nb_all \* 2 + 3) & ~3/nb_all * 2/' $D/csrc/dsd4w.hip
@@ -24,5 +24,5 @@ for f in block_gemm dsd4w metadata dispatch c_api; do
     -DSPUTNIK_BUILD_HASH=\"preload_bug\" -x hip -c $src -o $D/$f.o &
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/build/exp/preload_bug.so $D/*.o
-echo built $ROOT/build/exp/preload_bug.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $ROOT/build/bug/preload_bug.so $D/*.o
+echo built $ROOT/build/bug/preload_bug.so

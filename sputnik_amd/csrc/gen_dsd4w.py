@@ -850,6 +850,13 @@ def render():
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W4 \\")
         lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, ds=True, il=True)]
         lines += ['  ""', ""]
+        # the shipped DSD NN variants (_W2, _W4) with timeline stamps
+        # (experiment builds, SPUTNIK_EXP & 512)
+        for name, il in (("_W2_T", False), ("_W4_T", True)):
+            lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
+            lines += [f'  "{ins}\\n" \\'
+                      for ins in build(dt, True, False, True, ds=True, il=il)]
+            lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),
                               ("_W3_SDD_NT", True, True)):
