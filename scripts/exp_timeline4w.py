@@ -32,9 +32,19 @@ def stats(v):
 
 
 def main():
-    dens = [float(x) for x in (sys.argv[1:] or ["0.5", "0.1", "0.9"])]
+    # arguments: densities, and mode=N for the kernel variant
+    # (sputnik_select_dsd_kernel; default 1, the shipped choice)
+    mode = 1
+    args = []
+    for a in sys.argv[1:]:
+        if a.startswith("mode="):
+            mode = int(a[5:])
+        else:
+            args.append(a)
+    dens = [float(x) for x in (args or ["0.5", "0.1", "0.9"])]
     dev = torch.device("cuda", 0)
     L = sp.lib()
+    sp.select_dsd_kernel(mode)
     L.sputnik_exp_set_debug.argtypes = [ctypes.c_void_p]
     buf = torch.zeros(16 * 4096, dtype=torch.int64, device=dev)
     for d in dens:
@@ -57,7 +67,7 @@ def main():
         e0 = t[:, 0].min()
         us = lambda x: x / 100.0  # noqa: E731
         role = t[:, 6]  # 1 producer, 2 consumer, 0 plain
-        out = {"density": d, "pair_xcd2": os.environ.get("SPUTNIK_AMD_PAIR_XCD2", "default"),
+        out = {"density": d, "mode": mode, "pair_xcd2": os.environ.get("SPUTNIK_AMD_PAIR_XCD2", "default"),
                "workgroups": int(len(t)),
                "span_us": round(us(t[:, 4].max() - e0), 2),
                "entry_skew_us": round(us(t[:, 0].max() - e0), 2),

@@ -23,8 +23,15 @@ tail -5 $OUT/bug_lib.log
 if [ -f $R/build/tlx/tl4.so ]; then
   echo "== timeline" | tee -a $OUT/steps.log
   SPUTNIK_AMD_LIB=$R/build/tlx/tl4.so timeout -k 10 300 python scripts/exp_timeline4w.py \
-    0.5 0.1 0.3 0.9 > $OUT/tl4.log 2>&1; rc3=$?
+    0.5 0.1 0.3 0.9 > $OUT/tl4.log 2>&1 && \
+  SPUTNIK_AMD_LIB=$R/build/tlx/tl4.so timeout -k 10 300 python scripts/exp_timeline4w.py \
+    0.5 0.1 0.3 0.9 mode=8 > $OUT/tl4_m8.log 2>&1; rc3=$?
   echo "== timeline rc=$rc3" | tee -a $OUT/steps.log
   [ $rc3 -ne 0 ] && exit $rc3
 fi
+echo "== ab" | tee -a $OUT/steps.log
+timeout -k 10 400 python scripts/ab_dsd4w.py --densities 0.5,0.1,0.3,0.9 --rounds 7 \
+  > $OUT/ab.jsonl 2> $OUT/ab.err; rc4=$?
+echo "== ab rc=$rc4" | tee -a $OUT/steps.log
+[ $rc4 -ne 0 ] && exit $rc4
 exit $rc
