@@ -193,12 +193,11 @@ int sputnik_capture_workspaces(void);
 void sputnik_debug_pair_fault(int on);
 /* Kernel choice for DSD / DDS (every transpose) and the grouped SDD: 1 =
  * the 4-wave hand-scheduled kernel where it applies and pays (the default),
- * 2..8 = wherever it applies, whatever the density, with the DSD NN variant
+ * 2..7 = wherever it applies, whatever the density, with the DSD NN variant
  * kEpi = mode - 2 (0 workgroup epilogue, 1 per-wave, 2 per-wave +
  * specialized last block, 3 double slots, 4 double slots + barrier every
- * other step + interleaved copy-out, 5 double slots + interleaved copy-out,
- * 6 double slots + epilogue stored straight from registers;
- * DDS NN runs kEpi 1 for modes 2-4 and kEpi 3 for 5-8, the grouped SDD the
+ * other step + interleaved copy-out, 5 double slots + interleaved copy-out;
+ * DDS NN runs kEpi 1 for modes 2-4 and kEpi 3 for 5-7, the grouped SDD the
  * barrier-every-other-step variant for mode 6 and double slots otherwise,
  * the transposed DSD / DDS launches the one variant they have), 0 = the
  * 8-wave kernel everywhere, -1 = query only. Returns the previous choice.

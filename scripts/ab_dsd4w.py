@@ -60,8 +60,7 @@ def main():
             return s.elapsed_time(e) * 1e3 / a.calls
 
         arms = ({"8wave": 0, "4wave": 5, "4wave_bar2": 6} if a.op == "sdd"
-                else {"8wave": 0, "4wave_ds": 5, "4wave_bar2": 6, "4wave_il": 7,
-                      "4wave_direct": 8})
+                else {"8wave": 0, "4wave_ds": 5, "4wave_bar2": 6, "4wave_il": 7})
         for mode in arms.values():
             timed(mode)
             for _ in range(100):

@@ -23,9 +23,7 @@ tail -5 $OUT/bug_lib.log
 if [ -f $R/build/tlx/tl4.so ]; then
   echo "== timeline" | tee -a $OUT/steps.log
   SPUTNIK_AMD_LIB=$R/build/tlx/tl4.so timeout -k 10 300 python scripts/exp_timeline4w.py \
-    0.5 0.1 0.3 0.9 > $OUT/tl4.log 2>&1 && \
-  SPUTNIK_AMD_LIB=$R/build/tlx/tl4.so timeout -k 10 300 python scripts/exp_timeline4w.py \
-    0.5 0.1 0.3 0.9 mode=8 > $OUT/tl4_m8.log 2>&1; rc3=$?
+    0.5 0.1 0.3 0.9 > $OUT/tl4.log 2>&1; rc3=$?
   echo "== timeline rc=$rc3" | tee -a $OUT/steps.log
   [ $rc3 -ne 0 ] && exit $rc3
 fi

@@ -432,12 +432,11 @@ def dsd_plan(a, transpose_a, b, transpose_b, c, stream=None) -> int:
 
 def select_dsd_kernel(four_wave: int = -1) -> int:
     """DSD / DDS / grouped-SDD kernel choice (sputnik_select_dsd_kernel): 1
-    the 4-wave hand-scheduled kernel where it pays (default), 2-8 wherever
+    the 4-wave hand-scheduled kernel where it pays (default), 2-7 wherever
     it applies with a fixed variant (kEpi = mode - 2: 0 workgroup epilogue,
     1 per-wave, 2 specialized last block, 3 double slots, 4 double slots +
     barrier every other step + interleaved copy-out, 5 double slots +
-    interleaved copy-out, 6 double slots + epilogue straight from
-    registers; transposed and SDD launches take the variant they
+    interleaved copy-out; transposed and SDD launches take the variant they
     have), 0 the 8-wave kernel, -1 query only. Returns the previous
     choice."""
     return int(lib().sputnik_select_dsd_kernel(int(four_wave)))

@@ -103,7 +103,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"pair_xcd2", "SPUTNIK_AMD_PAIR_XCD2", 3, 0, 3},
     {"split", "SPUTNIK_AMD_SPLIT", 1, 0, 1},
     {"split_min_bn", "SPUTNIK_AMD_SPLIT_MIN_BN", 128, 0, 1 << 20},
-    {"dsd4w", "SPUTNIK_AMD_DSD4W", 1, 0, 8},
+    {"dsd4w", "SPUTNIK_AMD_DSD4W", 1, 0, 7},
     {"grouped_sdd", "SPUTNIK_AMD_GROUPED_SDD", 1, 0, 1},
     {"grouped_min_per_cu", "SPUTNIK_AMD_GROUPED_MIN_PER_CU", 5, 0, 1 << 20},
     {"tall", "SPUTNIK_AMD_TALL", 1, 0, 2},
@@ -474,8 +474,8 @@ void SetPairFault(int on) { (void)TuningSet("pair_fault", on != 0 ? 1 : 0); }
 // A/B) keeps the 8-wave kernel.
 static int Dsd4wMode() { return Knob(kKnobDsd4w); }
 bool Dsd4wEnabled() { return Dsd4wMode() != 0; }
-// 2..8: wherever the kernel can run, whatever the density (tests, A/B), with
-// epilogue 0 .. 6 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
+// 2..7: wherever the kernel can run, whatever the density (tests, A/B), with
+// epilogue 0 .. 5 (dsd4w.h LaunchDsd4w); 1: the default epilogue.
 bool Dsd4wForced() { return Dsd4wMode() >= 2; }
 int Dsd4wEpi() {
   const int m = Dsd4wMode();
@@ -483,7 +483,7 @@ int Dsd4wEpi() {
 }
 int SelectDsdKernel(int four_wave) {
   if (four_wave < 0) return Dsd4wMode();
-  return TuningSet("dsd4w", four_wave > 8 ? 8 : four_wave);
+  return TuningSet("dsd4w", four_wave > 7 ? 7 : four_wave);
 }
 
 static void ReclaimCaptureSlots() {

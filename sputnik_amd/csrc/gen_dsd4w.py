@@ -43,8 +43,7 @@ Everything read-only comes in as an operand (%[name]); %[flags] packs the
 workgroup's role bits: 0 collect (pair consumer), 1 specialized last block
 allowed, 2 test fault (producer skips its flag), 3 last wave (raises the
 flag), 4 wave 0 (counts a time-out), 5 split-mode first chunk (no tile of
-its own: ends after publishing), 6 the wave's 128 columns all inside C (the
-direct epilogue may run).
+its own: ends after publishing).
 
 Sparse-row segments (pair balancing, dispatch.cpp PreparePairs): a virtual
 entry x in [0, ntot) is the CSR entry x + (x < n1 ? b1 : b2m) (b2m = b2 - n1).
@@ -125,11 +124,7 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False, "tn": False, "ddstt": False, "il": False, "direct": False}
-# "direct": the per-wave epilogue stores straight from registers
-# (epilogue_direct; a pair consumer folds the partial into its accumulators
-# first, fold_partial) when the wave's 128 columns lie inside C (flags bit
-# 6), else the staged epilogue (_W5, DSD NN with double slots).
+           "bar2": False, "tn": False, "ddstt": False, "il": False}
 # "il": the plain per-wave epilogue stores each 16-row batch as soon as it is
 # staged (on with "bar2"; alone: _W4).
 # DDS TT ("ddstt", with "ds"): B's rows (storage order) are the shared image
@@ -233,9 +228,13 @@ def idx_load():
     if col_order():
         out += ["s_lshl_b32 s74, s79, 2", "s_add_u32 s74, %[bolo], s74",
                 "s_addc_u32 s75, %[bohi], 0", "s_load_dword s62, s[74:75], 0x0"]
-    return out + ["s_lshl_b32 s79, s79, 1", "s_and_b32 s60, s79, 2",
-                  "s_lshl_b32 s60, s60, 3", "s_and_b32 s79, s79, 0xfffffffc",
+    # the entry's byte address, then its aligned dword and the half within
+    # it (the list may start 2 bytes into a dword: a scalar load drops the
+    # low address bits, block_gemm.h scalar_load_short)
+    return out + ["s_lshl_b32 s79, s79, 1",
                   "s_add_u32 s76, %[ixlo], s79", "s_addc_u32 s77, %[ixhi], 0",
+                  "s_and_b32 s60, s76, 2", "s_lshl_b32 s60, s60, 3",
+                  "s_and_b32 s76, s76, 0xfffffffc",
                   "s_load_dword s59, s[76:77], 0x0"]
 
 
@@ -684,119 +683,42 @@ def copy_out():
     return out
 
 
-def poll(tag=""):
+def poll():
     """Consumer: wait (bounded, s_memrealtime) for the producer's flag =
     this launch's epoch; every wave polls for itself (each adds only its own
     part of the partial). On time-out wave 0 counts the error and the tile
-    becomes NaN. (tag: label suffix of a second copy, the direct epilogue's)"""
+    becomes NaN."""
     return ["s_memrealtime s[96:97]", "s_waitcnt lgkmcnt(0)",
-            f"L_poll{tag}_%=:",
+            "L_poll_%=:",
             "v_mov_b32 v96, 0",
             "global_load_dword v97, v96, %[flag] sc1",
             "s_waitcnt vmcnt(0)", "s_nop 0",
             "v_readfirstlane_b32 s98, v97",
-            "s_cmp_eq_u32 s98, %[epoch]", f"s_cbranch_scc1 L_got{tag}_%=",
+            "s_cmp_eq_u32 s98, %[epoch]", "s_cbranch_scc1 L_got_%=",
             "s_sleep 1",
             "s_memrealtime s[98:99]", "s_waitcnt lgkmcnt(0)",
             "s_sub_u32 s98, s98, s96", "s_subb_u32 s99, s99, s97",
-            "s_cmp_lg_u32 s99, 0", f"s_cbranch_scc1 L_timeout{tag}_%=",
-            f"s_cmp_lt_u32 s98, {WAIT_TICKS}", f"s_cbranch_scc1 L_poll{tag}_%=",
-            f"L_timeout{tag}_%=:",
-            "s_bitcmp1_b32 %[flags], 4", f"s_cbranch_scc0 L_nan{tag}_%=",
+            "s_cmp_lg_u32 s99, 0", "s_cbranch_scc1 L_timeout_%=",
+            f"s_cmp_lt_u32 s98, {WAIT_TICKS}", "s_cbranch_scc1 L_poll_%=",
+            "L_timeout_%=:",
+            "s_bitcmp1_b32 %[flags], 4", "s_cbranch_scc0 L_nan_%=",
             "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
             "v_mov_b32 v96, 0", "v_mov_b32 v97, 1",
             "global_atomic_add v96, v97, %[err]",
             "s_waitcnt vmcnt(0)",
             "s_mov_b64 exec, s[78:79]",
-            f"s_branch L_nan{tag}_%="]
-
-
-def fold_partial():
-    """Pair consumer, direct epilogue: the published fp32 partial added into
-    the accumulators (a[i] += partial, in place), streamed through v[128:255]
-    (32 fragments in flight, sc1 loads, as epilogue_body; only loads are in
-    flight, so the counted waits rely on nothing but in-order load returns).
-    The sums are the staged epilogue's exactly (acc + partial, fp32)."""
-    out = []
-
-    def load(i):
-        v = 128 + 4 * (i % 32)
-        return [f"s_mov_b32 s78, {(i // 4) * 4096}",
-                f"buffer_load_dwordx4 v[{v}:{v + 3}], %[vpl], s[84:87], s78 offen "
-                f"offset:{(i % 4) * 1024} sc1"]
-
-    for i in range(32):
-        out += load(i)
-    for i in range(64):
-        t = 96 + 8 * (i % 4)
-        out += [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
-        out.append(f"s_waitcnt vmcnt({min(31, 63 - i)})")
-        p = 128 + 4 * (i % 32)
-        out += [f"v_add_f32 v{t + j}, v{t + j}, v{p + j}" for j in range(4)]
-        if i + 32 < 64:
-            out += load(i + 32)
-        out += [f"v_accvgpr_write_b32 a{4 * i + j}, v{t + j}" for j in range(4)]
-    out += ["s_nop 7", "s_nop 7"]  # (VALU writes of a[] before their reads)
-    return out
-
-
-def epilogue_direct(cvt, mode):
-    """Accumulators -> C straight from registers (no LDS staging), for a wave
-    whose 128 columns all lie inside C (flags bit 6; otherwise the staged
-    epilogue runs). Tiles (m, n) and (m, n + 1) go out together: lane (r, g)
-    (r = l % 16, g = l / 16) holds 4 consecutive columns 16 n + 4 g .. + 3 of
-    row 16 m + r of each (the MFMA layout); after the fp16 / bf16 packing
-    (lo = columns + 0, + 1, hi = + 2, + 3), two v_permlane16_swap (odd lane
-    rows of the first operand <-> even lane rows of the second) leave lane
-    (r, g) with 16 contiguous bytes: tile n's columns 0-7 (g = 0) or 8-15
-    (g = 2), tile n + 1's columns 0-7 (g = 1) or 8-15 (g = 3) -- byte
-    32 n + {0, 32, 16, 48}[g] of the row (the lane part is in %[vcd]). One
-    16-byte nontemporal store per lane then writes 16 rows x 64 contiguous
-    bytes; the row batch 16 m ldc is in s78 (s79 = 16 ldc). Three register
-    sets (v[96:107], v[108:119], v[120:131]) rotate, so a store's data is
-    not overwritten before two other pairs' work. mode "plain" (a pair
-    consumer runs fold_partial first) or "nan"."""
-    out = ["s_mov_b32 s84, %[cdlo]", "s_mov_b32 s85, %[cdhi]",
-           "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
-           "s_mov_b32 s78, 0", "s_lshl_b32 s79, %[c4], 2"]
-    if mode == "nan":
-        nan = NAN_F16 if cvt.endswith("f16_f32") else NAN_BF16
-        out += [f"v_mov_b32 v{96 + j}, {nan}" for j in range(4)]
-        for m in range(8):
-            for j in range(4):
-                out.append(f"buffer_store_dwordx4 v[96:99], %[vcd], s[84:87], s78 "
-                           f"offen offset:{64 * j} nt")
-            out.append("s_add_u32 s78, s78, s79")
-        return out
-    for q in range(32):  # tile pair q: m = q / 4, n = 2 (q % 4)
-        m, n = q // 4, 2 * (q % 4)
-        i = 8 * m + n
-        s = 96 + 12 * (q % 3)
-        out += [f"v_accvgpr_read_b32 v{s + j}, a{4 * i + j}" for j in range(8)]
-        out += [f"{cvt} v{s + 8}, v{s}, v{s + 1}", f"{cvt} v{s + 9}, v{s + 2}, v{s + 3}",
-                f"{cvt} v{s + 10}, v{s + 4}, v{s + 5}",
-                f"{cvt} v{s + 11}, v{s + 6}, v{s + 7}",
-                "s_nop 1",
-                f"v_permlane16_swap_b32 v{s + 8}, v{s + 10}",
-                f"v_permlane16_swap_b32 v{s + 9}, v{s + 11}",
-                "s_nop 1",
-                f"buffer_store_dwordx4 v[{s + 8}:{s + 11}], %[vcd], s[84:87], s78 "
-                f"offen offset:{32 * n} nt"]
-        if q % 4 == 3:
-            out.append("s_add_u32 s78, s78, s79")
-    return out
+            "s_branch L_nan_%="]
 
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False,
-          direct=False):
+          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False):
     VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt,
-                   il=il, direct=direct)
+                   il=il)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
         VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
-                       tn=False, ddstt=False, il=False, direct=False)
+                       tn=False, ddstt=False, il=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -862,21 +784,6 @@ def _build(dt, wave_epi, last_block, stamps):
         # every DMA landed and every wave's reads are done: the LDS is free
         # for the staging image
         body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
-    if VARIANT["direct"]:
-        # flags bit 6: the wave's 128 columns all inside C -> straight from
-        # registers; otherwise the staged epilogue below
-        body += ["s_bitcmp1_b32 %[flags], 6", "s_cbranch_scc0 L_staged_%=",
-                 "s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc0 L_dplain_%="]
-        body += poll("d")
-        body.append("L_gotd_%=:")
-        body += fold_partial()
-        body.append("L_dplain_%=:")
-        body += epilogue_direct(cvt, "plain")
-        body.append("s_branch L_fin_%=")
-        body.append("L_nand_%=:")
-        body += epilogue_direct(cvt, "nan")
-        body.append("s_branch L_fin_%=")
-        body.append("L_staged_%=:")
     body += ["s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc1 L_collect_%="]
     if VARIANT["bar2"] or VARIANT["il"]:
         # (with bar2 / il: the plain epilogue stores each 16-row batch as
@@ -947,18 +854,12 @@ def render():
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W4 \\")
         lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, ds=True, il=True)]
         lines += ['  ""', ""]
-        # _W5: double slots with the direct epilogue (DSD)
-        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W5 \\")
-        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, ds=True, direct=True)]
-        lines += ['  ""', ""]
-        # the DSD NN variants (_W2, _W4, _W5) with timeline stamps
+        # the shipped DSD NN variants (_W2, _W4) with timeline stamps
         # (experiment builds, SPUTNIK_EXP & 512)
-        for name, il, direct in (("_W2_T", False, False), ("_W4_T", True, False),
-                                 ("_W5_T", False, True)):
+        for name, il in (("_W2_T", False), ("_W4_T", True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
-                      for ins in build(dt, True, False, True, ds=True, il=il,
-                                       direct=direct)]
+                      for ins in build(dt, True, False, True, ds=True, il=il)]
             lines += ['  ""', ""]
         # _W3*: double slots with a barrier every other step
         for name, sdd, nt in (("_W3", False, False), ("_W3_SDD", True, False),

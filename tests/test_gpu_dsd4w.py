@@ -52,9 +52,7 @@ def _run(A, B, m, n, dtype, mode, tb=False):
     3 with the per-wave epilogue, 4 per-wave + specialized last block, 5
     per-wave + double-slot S image, 6 the same with a barrier every other
     step and the interleaved epilogue, 7 double slots + the interleaved
-    epilogue, 8 double slots + the epilogue stored straight from registers
-    (the staged one for a wave with columns past N); 2-8 regardless of the
-    density gate."""
+    epilogue; 2-7 regardless of the density gate."""
     td = torch.float16 if dtype == "f16" else torch.bfloat16
     c = torch.full((m * n,), float("nan"), dtype=td, device="cuda")
     prev = sp.select_dsd_kernel(mode)
@@ -82,7 +80,7 @@ CASES = [
 
 @pytest.mark.parametrize("m,k,n,density", CASES)
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
-@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6, 7])
 def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     A, B, off, idx, a, b = _problem(m, k, n, density, dtype, seed=m + n + int(density * 100))
     c4 = _run(A, B, m, n, dtype, mode)
@@ -93,7 +91,7 @@ def test_dsd4w_bit_identical_to_8wave(m, k, n, density, dtype, mode):
     assert sp.pair_errors() == 0
 
 
-@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("mode", [2, 3, 4, 5, 6, 7])
 def test_dsd4w_empty_rows_and_oracle(mode):
     """Empty block-rows get zero tiles; sampled rows against the oracle."""
     m, k, n = 4096, 2048, 1024
@@ -118,7 +116,7 @@ def test_dsd4w_empty_rows_and_oracle(mode):
 
 def test_dsd4w_selector_roundtrip():
     prev = sp.select_dsd_kernel(-1)
-    assert prev in (0, 1, 2, 3, 4, 5, 6, 7, 8)
+    assert prev in (0, 1, 2, 3, 4, 5, 6, 7)
     assert sp.select_dsd_kernel(0) == prev
     assert sp.select_dsd_kernel(-1) == 0
     assert sp.select_dsd_kernel(prev) == 0

@@ -370,28 +370,18 @@ def _skewed_rows(rng, rows_b=32, cols_b=32):
     return offsets, indices
 
 
-@pytest.mark.parametrize("op,ta,tb,mode", [("dsd", False, False, 1),
-                                           ("dsd", False, False, 8),
-                                           ("dsd", True, False, 1),
-                                           ("dsd", False, True, 1),
-                                           ("dds", False, False, 1),
-                                           ("dds", False, True, 1)])
-def test_pair_timeout_fails_loudly(op, ta, tb, mode):
+@pytest.mark.parametrize("op,ta,tb", [("dsd", False, False),
+                                      ("dsd", True, False),
+                                      ("dsd", False, True),
+                                      ("dds", False, False),
+                                      ("dds", False, True)])
+def test_pair_timeout_fails_loudly(op, ta, tb):
     """A pair producer that never publishes (test knob) makes its consumer
     time out (after the bounded wait): the consumer's tile is NaN (never a
     stale or partial sum), every such consumer is counted by
     sputnik_pair_errors(), the tiles without a hand-off are exact, and the
     next launch on the same workspace is exact and error-free again
-    (per-launch epochs, no flag to reset). mode 8: DSD NN with the
-    epilogue stored straight from registers (its own poll / NaN path)."""
-    prev_mode = sp.select_dsd_kernel(mode)
-    try:
-        _pair_timeout(op, ta, tb)
-    finally:
-        sp.select_dsd_kernel(prev_mode)
-
-
-def _pair_timeout(op, ta, tb):
+    (per-launch epochs, no flag to reset)."""
     rng = np.random.default_rng(5)
     topo = _skewed_rows(rng)
     if op == "dsd":
