@@ -398,21 +398,28 @@ def own_reads_kc(d, half, s):
             f"offset:{d * DS_SLOT + n * 2048}" for n in range(8)]
 
 
-def step_ds(dt, H, zero_c=False):
+def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
     """Step H of a block in double-slot mode: as step(), with the per-step
     image's DMAs of step + 3 every step and the double slot of steps + 3 and
     + 4 on odd H (fed steps 0-1 / 2-3 of a block). At gap 1 every DMA of
     step - 2 has landed (in-order vmcnt: step - 1's may fly), which covers
     both images of step + 1. The shared double slot of DSD is refilled only
     after this step's barrier: its previous steps were read up to the step
-    before (every wave has finished that step once all passed the barrier)."""
+    before (every wave has finished that step once all passed the barrier).
+    (Early publish, publish_sequence: `wait` overrides the gap-1 count,
+    `stores` adds (gap, instruction) pairs after the gap's own work, `flag`
+    raises the pair flag after the barrier, `pre` (gap, instruction) pairs
+    before it.)"""
     dds = VARIANT["dds"]
     cur, nxt = H % 2, 1 - H % 2
     gaps = [[] for _ in range(64)]
     if H == 0:
         gaps[0] += idx_load()
     n_odd, n_even = ds_counts()
-    gaps[1].append(f"s_waitcnt vmcnt({n_odd if (H - 1) % 2 == 1 else n_even})")
+    for g, ins in pre:
+        gaps[g].append(ins)
+    w = wait if wait is not None else (n_odd if (H - 1) % 2 == 1 else n_even)
+    gaps[1].append(f"s_waitcnt vmcnt({w})")
     if H == 1:
         gaps[1] += switch()
     s1 = (H + 1) % 4
@@ -434,6 +441,8 @@ def step_ds(dt, H, zero_c=False):
     bar = READS_AT + len(own)
     if not (VARIANT["bar2"] and not dds and not VARIANT["tt"] and H % 2 == 0):
         gaps[bar].append("s_barrier")
+        if flag:
+            gaps[bar] += raise_flag("e")
     for i, ins in enumerate(shared):
         gaps[bar + 1 + i].append(ins)
     fed = (H + 3) % 4
@@ -458,12 +467,101 @@ def step_ds(dt, H, zero_c=False):
         gaps[adv] += advance_per_step()
     if H == 1:
         gaps[adv] += advance_ds()
+    for g, ins in stores:
+        gaps[g].append(ins)
     gaps[63].append("s_waitcnt lgkmcnt(0)")
     out = []
     for i in range(64):
         out.append(mfma(dt, i // 8, i % 8, cur, zero_c))
         out += gaps[i]
     return out
+
+
+def raise_flag(tag=""):
+    """The last wave's lane 0 stores this launch's epoch into the pair flag
+    (sc1), unless the test fault bit is set (publish's tail)."""
+    return ["s_bitcmp1_b32 %[flags], 3", f"s_cbranch_scc0 L_noflag{tag}_%=",
+            "s_bitcmp1_b32 %[flags], 2", f"s_cbranch_scc1 L_noflag{tag}_%=",
+            "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+            "v_mov_b32 v96, 0", "v_mov_b32 v97, %[epoch]",
+            "global_store_dword v96, v97, %[flag] sc1",
+            "s_mov_b64 exec, s[78:79]",
+            f"L_noflag{tag}_%=:"]
+
+
+def _is_vmem(ins):
+    return ins.startswith(("buffer_load", "buffer_store", "global_"))
+
+
+def publish_sequence(dt):
+    """Early publish (double-slot variants; a pair producer whose own row
+    follows its head, %[pubat] = n2 + 1): the head's last block's step 3
+    stores every accumulator tile of the head partial as soon as its last
+    MFMA is 8 slots behind (sc1, from the AGPRs, per-lane address v[96 +
+    i / 4] = %[vpl] + 4 KiB (i / 4)), the rest in the gaps of the next
+    block's step 0 before that step's zero-C MFMAs overwrite them; the
+    k-loop runs on meanwhile. vmcnt counts loads, stores and LDS-DMA
+    together in issue order (MI355X_MICROARCH.md, s_waitcnt), so each step's
+    wait is recounted here over the actual instruction stream: all but the
+    operations younger than the last DMA of the step two back. The first
+    step whose wait leaves no store younger than that DMA has every store of
+    the wave complete; after its barrier (every wave passed its own wait)
+    the last wave raises the flag. Returns (instructions, rejoin label)."""
+    n_odd, n_even = ds_counts()
+    k1 = 63 - n_odd  # stores in step 3 (vmcnt counts to 63)
+
+    def store(i):
+        return (f"buffer_store_dwordx4 a[{4 * i}:{4 * i + 3}], v{96 + i // 4}, s[84:87], 0 "
+                f"offen offset:{(i % 4) * 1024} sc1")
+    pre = [(2 + j // 3, f"v_add_u32 v{96 + j}, {j * 4096}, %[vpl]") for j in range(16)]
+    specs = [dict(H=3, stores=[(i + 8, store(i)) for i in range(k1)], pre=pre),
+             dict(H=0, zero_c=True, stores=[(2 + j, store(k1 + j)) for j in range(64 - k1)])]
+    for H in (1, 2, 3, 0, 1):
+        specs.append(dict(H=H))
+    steps = []
+    for j, sp in enumerate(specs):
+        ins = step_ds(dt, sp["H"], sp.get("zero_c", False), wait=None if j == 0 else 999,
+                      stores=sp.get("stores", ()), pre=sp.get("pre", ()))
+        steps.append(ins)
+    # recount the waits of steps 1.. (step 0's is the loop's own)
+    out_steps = [steps[0]]
+    flag_at = None
+    for j in range(1, len(specs)):
+        # the youngest DMA at or before step j - 2 (a step may issue none:
+        # NT's even steps); everything issued after it may still fly
+        younger = []
+        for t in range(j - 1, -1, -1):
+            dmas_t = [k for k, x in enumerate(steps[t]) if x.startswith("buffer_load")
+                      and x.endswith("lds")]
+            if t <= j - 2 and dmas_t:
+                younger = [x for x in steps[t][dmas_t[-1] + 1:] if _is_vmem(x)] + younger
+                break
+            younger = [x for x in steps[t] if _is_vmem(x)] + younger
+        w = len(younger)
+        assert w <= 63, w
+        stores_younger = any(x.startswith("buffer_store") for x in younger)
+        sp = specs[j]
+        flag = not stores_younger
+        ins = step_ds(dt, sp["H"], sp.get("zero_c", False), wait=w,
+                      stores=sp.get("stores", ()), flag=flag)
+        steps[j] = ins
+        out_steps.append(ins)
+        if flag:
+            flag_at = j
+            break
+    # the flag must be up before the producer's own row can end (its first
+    # block ends with the sequence's first step 3)
+    assert flag_at is not None and flag_at <= 4, flag_at
+    body = []
+    for j, ins in enumerate(out_steps):
+        body += ins
+        if j == 0:
+            body.append("s_sub_u32 s61, s61, 1")
+        elif specs[j]["H"] == 3:
+            body += ["s_sub_u32 s61, s61, 1", "s_cmp_lg_u32 s61, 0",
+                     "s_cbranch_scc0 L_exit_%="]
+    nxt = (specs[flag_at]["H"] + 1) % 4
+    return body, {0: "L_loop_%=", 1: "L_mid_%=", 2: "L_s2_%=", 3: "L_s3_%="}[nxt]
 
 
 def prologue_ds():
@@ -731,10 +829,18 @@ def _build(dt, wave_epi, last_block, stamps):
         body.append("s_memrealtime %[r0]")
     # the first block's step 0 is the zero-C copy below (L_first)
     body.append("s_branch L_first_%=")
+    # early publish (publish_sequence): double-slot variants with pairs
+    early = VARIANT["ds"] and not VARIANT["bar2"] and not VARIANT["sdd"]
     body.append("L_loop_%=:")
     body += step(dt, 0)
     body.append("L_mid_%=:")
     for H in (1, 2, 3):
+        if H == 2:
+            body.append("L_s2_%=:")
+        if H == 3:
+            if early:  # the head's last block of a producer with a row of its own
+                body += ["s_cmp_eq_u32 s61, %[pubat]", "s_cbranch_scc1 L_pubs_%="]
+            body.append("L_s3_%=:")
         body += step(dt, H)
     body += ["s_sub_u32 s61, s61, 1",
              "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%="]
@@ -755,6 +861,11 @@ def _build(dt, wave_epi, last_block, stamps):
             body += step(dt, H, last=H, cvt=cvt)
         body += ["s_nop 7", "s_nop 7"] + convert(cvt, 62) + convert(cvt, 63)
         body.append("s_branch L_done_%=")
+    if early:
+        seq, rejoin = publish_sequence(dt)
+        body.append("L_pubs_%=:")
+        body += seq
+        body.append(f"s_branch {rejoin}")
     body.append("L_pub_%=:")
     if stamps:
         body += ["s_memrealtime %[r3]", "s_waitcnt lgkmcnt(0)"]
