@@ -398,7 +398,8 @@ def own_reads_kc(d, half, s):
             f"offset:{d * DS_SLOT + n * 2048}" for n in range(8)]
 
 
-def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
+def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=(),
+            no_dma=False, no_reads=False):
     """Step H of a block in double-slot mode: as step(), with the per-step
     image's DMAs of step + 3 every step and the double slot of steps + 3 and
     + 4 on odd H (fed steps 0-1 / 2-3 of a block). At gap 1 every DMA of
@@ -409,7 +410,9 @@ def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
     (Early publish, publish_sequence: `wait` overrides the gap-1 count,
     `stores` adds (gap, instruction) pairs after the gap's own work, `flag`
     raises the pair flag after the barrier, `pre` (gap, instruction) pairs
-    before it.)"""
+    before it. Consumer last block, consumer_last_block: `no_dma` drops the
+    step's DMAs (they would feed steps past the row's end), `no_reads` its
+    fragment reads (the step after does not exist), `wait` -1 no wait.)"""
     dds = VARIANT["dds"]
     cur, nxt = H % 2, 1 - H % 2
     gaps = [[] for _ in range(64)]
@@ -419,7 +422,8 @@ def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
     for g, ins in pre:
         gaps[g].append(ins)
     w = wait if wait is not None else (n_odd if (H - 1) % 2 == 1 else n_even)
-    gaps[1].append(f"s_waitcnt vmcnt({w})")
+    if w >= 0:
+        gaps[1].append(f"s_waitcnt vmcnt({w})")
     if H == 1:
         gaps[1] += switch()
     s1 = (H + 1) % 4
@@ -436,6 +440,8 @@ def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
     else:
         tr = d_reads(s1, nxt)
         own, shared = (kc, tr) if dds else (tr, kc)
+    if no_reads:
+        own, shared = [], []
     for i, ins in enumerate(own):
         gaps[READS_AT + i].append(ins)
     bar = READS_AT + len(own)
@@ -459,6 +465,8 @@ def step_ds(dt, H, zero_c=False, wait=None, stores=(), flag=False, pre=()):
         placed += list(zip(ds_dmas(fed // 2), pos_ds))
         if VARIANT["nt"]:
             placed += list(zip(own_ds_dmas(fed // 2), [3 + 3 * i for i in range(16)]))
+    if no_dma:
+        placed = []
     for (m0, ld), k in placed:
         gaps[k - 1].append(m0)
         gaps[k].append(ld)
@@ -562,6 +570,75 @@ def publish_sequence(dt):
                      "s_cbranch_scc0 L_exit_%="]
     nxt = (specs[flag_at]["H"] + 1) % 4
     return body, {0: "L_loop_%=", 1: "L_mid_%=", 2: "L_s2_%=", 3: "L_s3_%="}[nxt]
+
+
+def _pload(f):
+    """sc1 load of the pair partial's fragment f (1 KiB per wave) into slot
+    f % 32 = v[96 + 4 (f % 32)] (soffset s78 = 4 KiB (f / 4), set first)."""
+    v = 96 + 4 * (f % 32)
+    return [f"s_mov_b32 s78, {(f // 4) * 4096}",
+            f"buffer_load_dwordx4 v[{v}:{v + 3}], %[vpl], s[84:87], s78 offen "
+            f"offset:{(f % 4) * 1024} sc1"]
+
+
+def consumer_last_block(dt):
+    """Pair consumer, double-slot variants (%[clbf] = 2, %[clbc] = 1 for a
+    consumer of at least 3 blocks, 0 otherwise): the flag is loaded (sc1)
+    when the penultimate block starts; when the last block starts that load
+    is four steps old (a counted wait), and if the producer has published,
+    the last block runs here: its steps 1-3 issue no DMA (each would feed a
+    step past the row's end), step 3 no fragment reads, and the partial's
+    fragments 0-7 (step 1, into v[96:127], free during the k-loop) and 8-23
+    (step 3, into fragment set 0, v[128:191], free once step 2's MFMAs are 8
+    slots behind) are loaded (sc1, after the matched poll, as the hand-off
+    table requires) while the MFMAs run. The epilogue (epilogue_collect_pre)
+    then needs no poll and no DMA drain. Otherwise the normal last block and
+    the polling epilogue run. Returns (flag-load code, check code, last
+    block)."""
+    flag_load = ["v_mov_b32 v96, 0", "global_load_dword v97, v96, %[flag] sc1"]
+    # VMEM ops issued after the flag load: the penultimate block's DMAs
+    n_odd, n_even = ds_counts()
+    k = 2 * (n_odd + n_even)
+    check = [f"s_waitcnt vmcnt({k})", "v_readfirstlane_b32 s98, v97",
+             "s_cmp_eq_u32 s98, %[epoch]", "s_cbranch_scc0 L_loop_%="]
+    loads1 = []
+    for f in range(8):
+        loads1 += [(4 + 2 * f, x) for x in _pload(f)]
+    loads3 = []
+    for f in range(8, 24):
+        loads3 += [(8 + 2 * (f - 8), x) for x in _pload(f)]
+    body = step_ds(dt, 0)
+    # step 1 waits for step 3 of the penultimate block (step 0's DMAs fly)
+    body += step_ds(dt, 1, wait=n_even, stores=loads1, no_dma=True)
+    # step 2 needs step 0's DMAs: every DMA is older than step 1's 8 loads
+    body += step_ds(dt, 2, wait=8, no_dma=True)
+    # step 3 reads nothing: no wait
+    body += step_ds(dt, 3, wait=-1, stores=loads3, no_dma=True, no_reads=True)
+    return flag_load, check, body
+
+
+def epilogue_collect_pre(cvt):
+    """Epilogue of a consumer that ran consumer_last_block: fragments 0-23
+    of the partial are in v[96:191] (in flight or landed), 24-31 are loaded
+    now into v[192:223]; tile i adds slot i % 32 and refills it with
+    fragment i + 32; temporaries v[224:255]. Only these loads are in flight
+    (the block issued no DMA), in issue order f = 0, 1, ... 63, so tile i
+    waits for vmcnt(min(31, 63 - i)) as epilogue_body. Staging and the sums
+    are epilogue_body's (acc + partial, the same fp32 additions)."""
+    out = []
+    for f in range(24, 32):
+        out += _pload(f)
+    for i in range(64):
+        t = 224 + 8 * (i % 4)
+        out += [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
+        out.append(f"s_waitcnt vmcnt({min(31, 63 - i)})")
+        p = 96 + 4 * (i % 32)
+        out += [f"v_add_f32 v{t + j}, v{t + j}, v{p + j}" for j in range(4)]
+        if i + 32 < 64:
+            out += _pload(i + 32)
+        out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}",
+                f"ds_write_b64 %[vws{i % 8}], v[{t + 4}:{t + 5}] offset:{4096 * (i // 8)}"]
+    return out
 
 
 def prologue_ds():
@@ -844,6 +921,9 @@ def _build(dt, wave_epi, last_block, stamps):
         body += step(dt, H)
     body += ["s_sub_u32 s61, s61, 1",
              "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%="]
+    if early:  # pair consumer: flag load / consumer last block
+        body += ["s_cmp_eq_u32 s61, %[clbf]", "s_cbranch_scc1 L_clbf_%=",
+                 "s_cmp_eq_u32 s61, %[clbc]", "s_cbranch_scc1 L_clbc_%="]
     if last_block:
         # one block left and no publish or collect after it: the
         # specialized last block (L_last)
@@ -866,6 +946,19 @@ def _build(dt, wave_epi, last_block, stamps):
         body.append("L_pubs_%=:")
         body += seq
         body.append(f"s_branch {rejoin}")
+        flag_load, check, clb = consumer_last_block(dt)
+        body.append("L_clbf_%=:")
+        body += flag_load
+        body.append("s_branch L_loop_%=")
+        body.append("L_clbc_%=:")
+        body += check
+        body += clb
+        if stamps:
+            body.append("s_memrealtime %[r1]")
+        # no DMA in flight, the wave's ring reads done (step 2's lgkmcnt)
+        body += ["s_nop 7", "s_nop 7"]
+        body += epilogue_collect_pre(cvt)
+        body.append("s_branch L_done_%=")
     body.append("L_pub_%=:")
     if stamps:
         body += ["s_memrealtime %[r3]", "s_waitcnt lgkmcnt(0)"]
