@@ -581,6 +581,28 @@ def _pload(f):
             f"offset:{(f % 4) * 1024} sc1"]
 
 
+def publish_last(dt, stamps=False):
+    """A producer with nothing after its head (a pair producer whose own row
+    is empty, a split-mode first chunk; %[publast] = 1): the head's last step
+    stores the partial's tiles 0-55 as each is final (sc1, 8 MFMA slots
+    behind, as publish_sequence), tiles 56-63 follow the step, then every
+    store drained, one barrier, and the last wave's flag -- the flag goes up
+    about a step after the last MFMA instead of after a 256 KiB publish."""
+    def store(i):
+        return (f"buffer_store_dwordx4 a[{4 * i}:{4 * i + 3}], v{96 + i // 4}, s[84:87], 0 "
+                f"offen offset:{(i % 4) * 1024} sc1")
+    pre = [(2 + j // 3, f"v_add_u32 v{96 + j}, {j * 4096}, %[vpl]") for j in range(16)]
+    out = ["s_memrealtime %[r3]", "s_waitcnt lgkmcnt(0)"] if stamps else []
+    out += step_ds(dt, 3, stores=[(i + 8, store(i)) for i in range(56)], pre=pre)
+    out += ["s_nop 7", "s_nop 7", "s_nop 7"]
+    out += [store(i) for i in range(56, 64)]
+    out += ["s_waitcnt vmcnt(0)", "s_barrier"] + raise_flag("l")
+    if stamps:
+        out += ["s_memrealtime %[r4]", "s_waitcnt lgkmcnt(0)"]
+    out += ["s_sub_u32 s61, s61, 1"]
+    return out
+
+
 def consumer_last_block(dt):
     """Pair consumer, double-slot variants (%[clbf] = 2, %[clbc] = 1 for a
     consumer of at least 3 blocks, 0 otherwise): the flag is loaded (sc1)
@@ -915,8 +937,9 @@ def _build(dt, wave_epi, last_block, stamps):
         if H == 2:
             body.append("L_s2_%=:")
         if H == 3:
-            if early:  # the head's last block of a producer with a row of its own
-                body += ["s_cmp_eq_u32 s61, %[pubat]", "s_cbranch_scc1 L_pubs_%="]
+            if early:  # the head's last block of a producer (own row after it / none)
+                body += ["s_cmp_eq_u32 s61, %[pubat]", "s_cbranch_scc1 L_pubs_%=",
+                         "s_cmp_eq_u32 s61, %[publast]", "s_cbranch_scc1 L_publ_%="]
             body.append("L_s3_%=:")
         body += step(dt, H)
     body += ["s_sub_u32 s61, s61, 1",
@@ -946,6 +969,9 @@ def _build(dt, wave_epi, last_block, stamps):
         body.append("L_pubs_%=:")
         body += seq
         body.append(f"s_branch {rejoin}")
+        body.append("L_publ_%=:")
+        body += publish_last(dt, stamps)
+        body.append("s_branch L_zero_%=")
         flag_load, check, clb = consumer_last_block(dt)
         body.append("L_clbf_%=:")
         body += flag_load
