@@ -18,6 +18,12 @@ echo "== ab" | tee -a $OUT/steps.log
 bash scripts/exp_run.sh $TAG "0.5 0.1 0.3 0.9" "pair" > $OUT/ab.log 2>&1; rc=$?
 echo "== ab rc=$rc" | tee -a $OUT/steps.log
 [ $rc -ne 0 ] && exit $rc
+# split mode (the N = 2 strong-scaling panel, M = 2048)
+for d in 0.5 0.1; do
+  timeout -k 10 300 python scripts/exp_bench.py --m 2048 --density $d build/exp/*.so \
+    >> $OUT/exp.jsonl 2> $OUT/exp_m2048.err; rc=$?
+  [ $rc -ne 0 ] && exit $rc
+done
 if [ -f $R/build/tlx/tl4.so ]; then
   echo "== timeline" | tee -a $OUT/steps.log
   SPUTNIK_AMD_LIB=$R/build/tlx/tl4.so timeout -k 10 300 python scripts/exp_timeline4w.py \
