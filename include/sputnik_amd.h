@@ -155,8 +155,11 @@ const char *sputnik_version(void);
 const char *sputnik_build_hash(void);
 
 /* ---- Diagnostics (need a device) */
-/* SDD tile plan: 1 = grouped 128x512 tiles (>= 5 blocks per CU), 0 = one
- * k-split 128x128 block per workgroup, -1 = the problem is rejected. */
+/* SDD tile plan: 1 = grouped 128x512 tiles (>= 5 blocks per CU), 2 = the
+ * grouped tiles with each group's K split over 2-8 workgroups (SDD NN, few
+ * groups: one workgroup per CU), 0 = one k-split 128x128 block per
+ * workgroup, -1 = the problem is rejected. (Decides as a launch on the null
+ * stream would, allocating nothing.) */
 int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_block_matrix_t *c);

@@ -356,7 +356,8 @@ def FreeBitmaskBuffers(m: BlockMatrix):  # noqa: N802
 
 def sdd_plan(a, transpose_a, b, transpose_b, c) -> int:
     """SDD tile plan the dispatcher picks on the current device: 1 grouped
-    128x512 tiles, 0 one k-split block per workgroup, -1 rejected."""
+    128x512 tiles, 2 grouped tiles with each group's K split over 2-8
+    workgroups, 0 one k-split block per workgroup, -1 rejected."""
     ca, cb, cc = a._c(), b._c(), c._c()
     return int(lib().sputnik_sdd_plan(ctypes.byref(ca), int(bool(transpose_a)),
                                       ctypes.byref(cb), int(bool(transpose_b)),

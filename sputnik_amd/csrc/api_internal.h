@@ -87,6 +87,9 @@ enum KnobId {
   kKnobDdsXcd2,
   kKnobSdd4wMaxLd,
   kKnobPairFault,
+  kKnobSddKsplit,
+  kKnobSddKsplitMinK,
+  kKnobSddOrder,
   kNumKnobs
 };
 int Knob(KnobId k);

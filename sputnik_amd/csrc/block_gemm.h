@@ -198,6 +198,16 @@ struct GemmParams {
   // Stored blocks of the sparse operand S (DSD: A's nonzeros / 128^2); the
   // 4-wave DSD kernel preloads an index list this short (dsd4w.hip).
   int s_blocks;
+  // SDD K-split (4-wave grouped SDD NN with few groups, dispatch.cpp
+  // PrepareSddKsplit): up to this many workgroups per group, each a slice of
+  // K, reduced through the pair workspace (pair_partials: 256 KiB per
+  // workgroup; ks_flags: one flag per workgroup, pair_epoch / pair_sync /
+  // pair_error as pairs). 0 or 1: off.
+  int sdd_ksplit;
+  unsigned *ks_flags;
+  // Grouped SDD on the 4-wave kernel, every row the same group count:
+  // 0 group-major order, 1 blocks of 8 rows x 4 groups (dsd4w.hip).
+  int sdd_order;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

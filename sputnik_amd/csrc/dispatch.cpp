@@ -111,6 +111,9 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 0, 0, 3},
     {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 16384, 0, 1 << 30},
     {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
+    {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
+    {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
+    {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -285,6 +288,100 @@ static bool PairsEnabled() {
 #endif
 // dry: decide only (DsdPlan): no workspace is allocated, re-tied or
 // advanced, and the pointers stay null.
+// The pair workspace of (device, stream) -- or of the capture under way on
+// `stream` -- found, re-tied or allocated (caller holds g_pairs_mu). dry:
+// decide only; a slot that would be allocated is described in *dry_slot
+// and nothing is allocated, re-tied or advanced. nullptr: none available.
+static PairSlot *AcquirePairSlot(hipStream_t stream, bool dry, PairSlot *dry_slot,
+                                 int *capturing_out) {
+  unsigned long long capture = 0;
+  const int capturing = CaptureState(stream, &capture);
+  *capturing_out = capturing;
+  if (capturing < 0) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  PairSlot *table = capturing ? g_capture_pairs : g_pairs;
+  const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
+  for (int i = 0; i < n_table; ++i) {
+    PairSlot &s = table[i];
+    if (s.partials != nullptr && s.device == dev && s.stream == stream &&
+        s.capture == capture)
+      return &s;
+  }
+  // A capture-table slot whose graph is gone is re-tied to the graph being
+  // captured, memory and device epoch word as they are: the word only ever
+  // grows, so the flags the old graph left can never match a new launch, and
+  // its arrival count is back at zero (the last arriver of every launch
+  // resets it). No HIP free on this path (ADVICE r04: frees happen in
+  // sputnik_capture_workspaces()).
+  if (capturing) {
+    for (int i = 0; i < n_table; ++i) {
+      PairSlot &s = table[i];
+      if (s.partials != nullptr && s.device == dev &&
+          s.released.load(std::memory_order_acquire) != 0) {
+        if (dry) return &s;
+        s.stream = stream;
+        s.capture = capture;
+        s.released.store(0, std::memory_order_relaxed);
+        (void)TieToCapturedGraph(stream, &s.released);
+        return &s;
+      }
+    }
+  }
+  PairSlot *slot = nullptr;
+  for (int i = 0; i < n_table; ++i)
+    if (table[i].partials == nullptr) {
+      slot = &table[i];
+      break;
+    }
+  if (slot == nullptr) {
+    if (!dry) WarnSlotsFull(capturing ? 2 : 0);
+    return nullptr;
+  }
+  const int cus = DeviceCUs(dev);
+  if (cus <= 0) return nullptr;
+  const int slots = cus * CfgSparse::kWGs;
+  // Partial slots of 128 x 512 fp32 (256 KiB): one per resident workgroup
+  // (a pair uses one per pair, split mode one per tile, the SDD K-split one
+  // per workgroup): 64 MiB per workspace on MI355X. Flags: [pairs] pair
+  // flags, the error word, [epoch, count] (pair_sync), [slots] K-split flags.
+  const int pairs = slots / 2;
+  if (dry) {  // the workspace a launch would allocate
+    dry_slot->slots = slots;
+    dry_slot->pairs = pairs;
+    return dry_slot;
+  }
+  void *partials = nullptr, *flags = nullptr;
+  if (AllocZeroed(&partials, (size_t)slots * kBM * CfgSparse::kBN * sizeof(float), dev) !=
+      hipSuccess)
+    return nullptr;
+  if (AllocZeroed(&flags, (pairs + 3 + slots) * sizeof(unsigned), dev) != hipSuccess) {
+    FreeQuiet(partials);
+    return nullptr;
+  }
+  slot->device = dev;
+  slot->stream = stream;
+  slot->capture = capture;
+  slot->partials = static_cast<float *>(partials);
+  slot->flags = static_cast<unsigned *>(flags);
+  slot->pairs = pairs;
+  slot->slots = slots;
+  slot->released.store(0, std::memory_order_relaxed);
+  if (capturing) (void)TieToCapturedGraph(stream, &slot->released);
+  return slot;
+}
+
+// A new epoch and the workspace pointers for one launch.
+static void BindPairSlot(GemmParams *p, PairSlot *slot, int capturing) {
+  if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
+  p->pair_partials = slot->partials;
+  p->pair_flags = slot->flags;
+  p->pair_epoch = slot->epoch;
+  p->pair_error = slot->flags + slot->pairs;
+  p->pair_sync = capturing ? slot->flags + slot->pairs + 1 : nullptr;
+  p->ks_flags = slot->flags + slot->pairs + 3;
+}
+
 static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream,
                          bool dry = false) {
   p->pair = 0;
@@ -293,102 +390,14 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream,
   if (!PairsEnabled() || p->num_rows < 2 || p->num_rows > kLptRows) return;
   if (blocks * 4 < (long long)p->num_rows * SPUTNIK_PAIR_MIN_MEAN4) return;
   if (stream == hipStreamPerThread) return;  // many streams, one handle
-  unsigned long long capture = 0;
-  const int capturing = CaptureState(stream, &capture);
-  if (capturing < 0) return;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
   std::lock_guard<std::mutex> lock(g_pairs_mu);
-  PairSlot *table = capturing ? g_capture_pairs : g_pairs;
-  const int n_table = capturing ? kMaxCaptureSlots : kMaxPairSlots;
-  PairSlot *slot = nullptr;
-  for (int i = 0; i < n_table; ++i) {
-    PairSlot &s = table[i];
-    if (s.partials != nullptr && s.device == dev && s.stream == stream &&
-        s.capture == capture) {
-      slot = &s;
-      break;
-    }
-  }
-  // A capture-table slot whose graph is gone is re-tied to the graph being
-  // captured, memory and device epoch word as they are: the word only ever
-  // grows, so the flags the old graph left can never match a new launch, and
-  // its arrival count is back at zero (the last arriver of every launch
-  // resets it). No HIP free on this path (ADVICE r04: frees happen in
-  // sputnik_capture_workspaces()).
-  if (slot == nullptr && capturing) {
-    for (int i = 0; i < n_table; ++i) {
-      PairSlot &s = table[i];
-      if (s.partials != nullptr && s.device == dev &&
-          s.released.load(std::memory_order_acquire) != 0) {
-        if (dry) {
-          slot = &s;
-          break;
-        }
-        s.stream = stream;
-        s.capture = capture;
-        s.released.store(0, std::memory_order_relaxed);
-        (void)TieToCapturedGraph(stream, &s.released);
-        slot = &s;
-        break;
-      }
-    }
-  }
   PairSlot dry_slot;
-  if (slot == nullptr) {
-    for (int i = 0; i < n_table; ++i)
-      if (table[i].partials == nullptr) {
-        slot = &table[i];
-        break;
-      }
-    if (slot == nullptr) {
-      if (!dry) WarnSlotsFull(capturing ? 2 : 0);
-      return;
-    }
-    const int cus = DeviceCUs(dev);
-    if (cus <= 0) return;
-    const int slots = cus * CfgSparse::kWGs;
-    if (dry) {  // the workspace a launch would allocate
-      dry_slot.slots = slots;
-      dry_slot.pairs = slots / 2;
-      slot = &dry_slot;
-    } else {
-    // Partial slots: slots / 2 pairs, or one per tile in split mode (at most
-    // slots / 2 tiles). 128 x 256 KiB = 32 MiB per workspace on MI355X.
-    const int pairs = slots / 2;
-    void *partials = nullptr, *flags = nullptr;
-    if (AllocZeroed(&partials, (size_t)pairs * kBM * CfgSparse::kBN *
-                                   sizeof(float), dev) != hipSuccess)
-      return;
-    if (AllocZeroed(&flags, (pairs + 3) * sizeof(unsigned), dev) !=
-        hipSuccess) {
-      hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-      (void)hipFree(partials);
-      (void)hipThreadExchangeStreamCaptureMode(&mode);
-      return;
-    }
-    slot->device = dev;
-    slot->stream = stream;
-    slot->capture = capture;
-    slot->partials = static_cast<float *>(partials);
-    slot->flags = static_cast<unsigned *>(flags);
-    slot->pairs = pairs;
-    slot->slots = slots;
-    slot->released.store(0, std::memory_order_relaxed);
-    if (capturing) (void)TieToCapturedGraph(stream, &slot->released);
-    }
-  }
+  int capturing = 0;
+  PairSlot *slot = AcquirePairSlot(stream, dry, &dry_slot, &capturing);
+  if (slot == nullptr) return;
   if (p->num_tiles > slot->slots) return;
   p->pair = 1;
-  if (!dry) {
-    if (++slot->epoch == 0) slot->epoch = 1;  // 0 is the initial flag value
-    p->pair_partials = slot->partials;
-    p->pair_flags = slot->flags;
-    p->pair_epoch = slot->epoch;
-    p->pair_error = slot->flags + slot->pairs;
-    p->pair_sync = capturing ? slot->flags + slot->pairs + 1 : nullptr;
-  }
+  if (!dry) BindPairSlot(p, slot, capturing);
   p->pair_fault = Knob(kKnobPairFault);
   // Two panels x half the pairs per XCD (GemmParams::pair_xcd2) from a mean
   // of 8 blocks per row: DSD 4096^3 A/B (r02m) 30% / 50% / 90% +1.2 / +2.7
@@ -854,6 +863,57 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   return true;
 }
 
+// SDD NN with too few stored blocks for the grouped grid (UseGroupedSdd
+// false) and few enough groups that every group can take 2 or more
+// workgroups: the 4-wave grouped kernel with each group's K split over S in
+// {2, 4, 8} workgroups (GemmParams::sdd_ksplit, S chosen in-kernel from the
+// actual group count), the partials reduced through the pair workspace.
+// Grid = one workgroup per CU, all resident at once (one 160-KiB-LDS
+// workgroup fits a CU): every chunk of a group is running while its peers
+// wait for it.
+// dry: decide only (SddPlan), no workspace allocated, re-tied or advanced.
+static bool PrepareSddKsplit(GemmParams *p, const BlockMatrix &c, bool ta, bool tb,
+                             hipStream_t stream, bool dry = false) {
+  const int max_s = Knob(kKnobSddKsplit);
+  if (max_s < 2 || ta || tb || c.offsets == nullptr || !Dsd4wEnabled()) return false;
+  // From K = 6144 (knob sdd_ksplit_min_k): its fixed cost -- every chunk
+  // publishes (S - 1) / S of its fp32 tile and reads as much back, ~10 us of
+  // fabric traffic at 248 workgroups -- is paid back by the shorter k-loop
+  // only on long K (A/B r05 ks2, us, 8-wave k-split tile vs K-split: 205
+  // blocks of 4096^2 at K = 4096 40.2 vs 42.0 (S = 4), K = 8192 68.9 vs
+  // 62.9 (S = 8); 60 blocks of 2048 x 4096, K = 4096 30.8 vs 31.0; 300
+  // blocks, K = 2048 37.5 vs 38.0).
+  if (p->num_rows > kMaxGroupRows || p->k_limit < Knob(kKnobSddKsplitMinK) ||
+      p->k_limit % 128 != 0)
+    return false;
+  if (stream == hipStreamPerThread) return false;  // many streams, one handle
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const int cus = DeviceCUs(dev);
+  if (cus <= 0) return false;
+  // groups: sum over rows of ceil(n_r / 4) <= (blocks + 3 rows) / 4
+  const long long blocks = p->num_tiles;
+  const long long groups_ub = (blocks + 3LL * p->num_rows) / 4;
+  if (groups_ub * 2 > cus) return false;
+  const long long span = 32LL * p->d_ld + (long long)p->j_limit * 2;
+  if (span > kMaxLaneOffset) return false;
+  GemmParams q = *p;
+  q.c_offsets = static_cast<const int *>(c.offsets);
+  if (!Sdd4wApplies(q, true, ta, tb)) return false;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  PairSlot dry_slot;
+  int capturing = 0;
+  PairSlot *slot = AcquirePairSlot(stream, dry, &dry_slot, &capturing);
+  if (slot == nullptr || cus > slot->slots) return false;
+  *p = q;
+  p->num_tiles = cus;
+  p->pair = 1;  // (the epoch and capture protocol of pair launches)
+  if (!dry) BindPairSlot(p, slot, capturing);
+  p->pair_fault = Knob(kKnobPairFault);
+  p->sdd_ksplit = max_s;
+  return true;
+}
+
 // Tall sparse operands (more block-rows than the in-kernel row ranking
 // handles, so no LPT order and no pair balancing) have many more tiles than
 // CUs: they run on CfgTall, two workgroups per CU.
@@ -1021,8 +1081,12 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   if (st != Status::kOk) return hipSuccess;
   p.debug = g_debug;
   const bool grouped = UseGroupedSdd(&p, c, tb);
-  if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb))
+  if (!grouped && PrepareSddKsplit(&p, c, ta, tb, stream))
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
+  if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb)) {
+    p.sdd_order = Knob(kKnobSddOrder);
+    return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
+  }
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
                          grouped, p, stream);
 }
@@ -1294,7 +1358,8 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
   if (PrepareSdd(*static_cast<const Matrix *>(a), ta,
                  *static_cast<const Matrix *>(b), tb, cm, &p) != Status::kOk)
     return -1;
-  return UseGroupedSdd(&p, cm, tb) ? 1 : 0;
+  if (UseGroupedSdd(&p, cm, tb)) return 1;
+  return PrepareSddKsplit(&p, cm, ta, tb, nullptr, /*dry=*/true) ? 2 : 0;
 }
 
 // Which kernel RunDsd would launch for this problem on `stream` (no

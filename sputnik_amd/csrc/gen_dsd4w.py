@@ -124,7 +124,8 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False, "tn": False, "ddstt": False, "il": False}
+           "bar2": False, "tn": False, "ddstt": False, "il": False, "ks": False}
+# "ks": SDD K-split (ksplit_path): the epilogue of a chunk of a group's K.
 # "il": the plain per-wave epilogue stores each 16-row batch as soon as it is
 # staged (on with "bar2"; alone: _W4).
 # DDS TT ("ddstt", with "ds"): B's rows (storage order) are the shared image
@@ -907,15 +908,143 @@ def poll():
             "s_branch L_nan_%="]
 
 
+KS_CHUNKS = (2, 4, 8)
+
+
+def ksplit_path(cvt, S, g, stamps=False):
+    """SDD K-split epilogue (VARIANT "ks", dsd4w.hip): the S workgroups of a
+    group each ran K-chunk c of the same 128 x 512 tile; chunk g owns rows
+    [128 g / S, 128 (g + 1) / S) of every wave's block, i.e. accumulator
+    tiles [64 g / S, 64 (g + 1) / S) (row tile m = i / 8). Each wave stores
+    its other tiles (fp32, sc1) to the workgroup's slot (%[pdlo] = the
+    group's S slots of 256 KiB, chunk h at h * 256 KiB, wave w at 64 KiB w,
+    tile i at 1 KiB i: soffset + offset over %[vpl]), every wave drains, one
+    barrier, the last wave's lane 0 stores the epoch into flag h = g of the
+    group (%[flag] + 4 g, sc1): the pair publish protocol
+    (MI355X_MICROARCH.md hand-off table row 1). Then each wave polls the
+    other chunks' flags itself and adds their tiles of its rows, in
+    ascending chunk order after its own (a fixed order: the result does not
+    depend on which chunk finished first), stages them and stores its rows.
+    A wave past the group's count (flags bit 6) stores and loads nothing but
+    joins the barrier."""
+    T = 64 // S
+    own = list(range(g * T, (g + 1) * T))
+    peers = [h for h in range(S) if h != g]
+    tag = f"{S}_{g}"
+    out = [f"L_ks{tag}_%=:",
+           "s_bitcmp1_b32 %[flags], 6", f"s_cbranch_scc1 L_ksb{tag}_%="]
+    soff = None
+    for i in range(64):
+        if i in own:
+            continue
+        v = g * 262144 + (i // 4) * 4096
+        if v != soff:
+            out.append(f"s_mov_b32 s78, {v}")
+            soff = v
+        out.append(f"buffer_store_dwordx4 a[{4 * i}:{4 * i + 3}], %[vpl], s[84:87], s78 "
+                   f"offen offset:{(i % 4) * 1024} sc1")
+    out += [f"L_ksb{tag}_%=:", "s_waitcnt vmcnt(0)", "s_barrier",
+            "s_bitcmp1_b32 %[flags], 3", f"s_cbranch_scc0 L_ksnf{tag}_%=",
+            "s_bitcmp1_b32 %[flags], 2", f"s_cbranch_scc1 L_ksnf{tag}_%=",
+            "s_mov_b64 s[78:79], exec", "s_mov_b64 exec, 1",
+            "v_mov_b32 v96, 0", "v_mov_b32 v97, %[epoch]",
+            f"global_store_dword v96, v97, %[flag] offset:{4 * g} sc1",
+            "s_mov_b64 exec, s[78:79]",
+            f"L_ksnf{tag}_%=:"]
+    if stamps:
+        out += ["s_memrealtime %[r3]", "s_waitcnt lgkmcnt(0)"]
+    out += ["s_bitcmp1_b32 %[flags], 6", "s_cbranch_scc1 L_fin_%="]
+    # bounded poll of the other chunks' flags (as poll())
+    out += ["s_memrealtime s[96:97]", "s_waitcnt lgkmcnt(0)",
+            f"L_ksp{tag}_%=:", "v_mov_b32 v96, 0"]
+    out += [f"global_load_dword v{97 + k}, v96, %[flag] offset:{4 * h} sc1"
+            for k, h in enumerate(peers)]
+    out.append("s_waitcnt vmcnt(0)")
+    for k in range(len(peers)):
+        out += [f"v_readfirstlane_b32 s98, v{97 + k}", "s_cmp_eq_u32 s98, %[epoch]",
+                f"s_cbranch_scc0 L_ksw{tag}_%="]
+    out += [f"s_branch L_ksg{tag}_%=",
+            f"L_ksw{tag}_%=:", "s_sleep 1",
+            "s_memrealtime s[98:99]", "s_waitcnt lgkmcnt(0)",
+            "s_sub_u32 s98, s98, s96", "s_subb_u32 s99, s99, s97",
+            "s_cmp_lg_u32 s99, 0", "s_cbranch_scc1 L_timeout_%=",
+            f"s_cmp_lt_u32 s98, {WAIT_TICKS}", f"s_cbranch_scc1 L_ksp{tag}_%=",
+            "s_branch L_timeout_%=",
+            f"L_ksg{tag}_%=:"]
+    if stamps:
+        out += ["s_memrealtime %[r4]", "s_waitcnt lgkmcnt(0)"]
+    # the other chunks' tiles of this wave's rows: (tile, chunk) loads in
+    # order, 32 in flight in v[128:255]
+    loads = [(i, h) for i in own for h in peers]
+    L = len(loads)
+
+    def load(n):
+        i, h = loads[n]
+        v = 128 + 4 * (n % 32)
+        return [f"s_mov_b32 s78, {h * 262144 + (i // 4) * 4096}",
+                f"buffer_load_dwordx4 v[{v}:{v + 3}], %[vpl], s[84:87], s78 offen "
+                f"offset:{(i % 4) * 1024} sc1"]
+    for n in range(min(32, L)):
+        out += load(n)
+    n = 0
+    for x, i in enumerate(own):
+        t = 96 + 8 * (x % 4)
+        out += [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
+        for _ in peers:
+            issued = min(L, 32 + n)
+            out.append(f"s_waitcnt vmcnt({min(63, issued - n - 1)})")
+            p = 128 + 4 * (n % 32)
+            out += [f"v_add_f32 v{t + j}, v{t + j}, v{p + j}" for j in range(4)]
+            if n + 32 < L:
+                out += load(n + 32)
+            n += 1
+        m, c = i // 8, i % 8
+        out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}",
+                f"ds_write_b64 %[vws{c}], v[{t + 4}:{t + 5}] offset:{4096 * m}"]
+    # this chunk's rows of the staged block -> C (copy_out's batches b0..)
+    b0, nb = 8 * g // S, 8 // S
+    out += ["s_waitcnt lgkmcnt(0)",
+            "s_mov_b32 s84, %[cdlo]", "s_mov_b32 s85, %[cdhi]",
+            "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000",
+            f"s_mul_i32 s78, %[c4], {4 * b0}"]
+    for b in range(b0, b0 + nb):
+        base = 96 + 16 * (b % 2)
+        for j in range(4):
+            out.append(f"ds_read_b128 v[{base + 4 * j}:{base + 4 * j + 3}], "
+                       f"%[vrb{j}] offset:{4096 * b}")
+        out.append("s_waitcnt lgkmcnt(0)")
+        for j in range(4):
+            out += [f"buffer_store_dwordx4 v[{base + 4 * j}:{base + 4 * j + 3}], %[vco], "
+                    f"s[84:87], s78 offen nt",
+                    "s_add_u32 s78, s78, %[c4]"]
+        out.append("s_nop 1")
+    out.append("s_branch L_fin_%=")
+    return out
+
+
+def ksplit():
+    """Dispatch on %[kss] (S) and %[kch] (this workgroup's chunk), then the
+    paths."""
+    out = ["L_ks_%=:"]
+    for S in KS_CHUNKS:
+        for g in range(S):
+            out += [f"s_cmp_eq_u32 %[kss], {S}", f"s_cbranch_scc0 L_ksn{S}_{g}_%=",
+                    f"s_cmp_eq_u32 %[kch], {g}", f"s_cbranch_scc1 L_ks{S}_{g}_%=",
+                    f"L_ksn{S}_{g}_%=:"]
+    out.append("s_branch L_fin_%=")  # (never: kss is one of KS_CHUNKS here)
+    return out
+
+
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
-          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False):
+          sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False,
+          ks=False):
     VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt,
-                   il=il)
+                   il=il, ks=ks)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
         VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
-                       tn=False, ddstt=False, il=False)
+                       tn=False, ddstt=False, il=False, ks=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -1014,6 +1143,8 @@ def _build(dt, wave_epi, last_block, stamps):
         # every DMA landed and every wave's reads are done: the LDS is free
         # for the staging image
         body += ["s_waitcnt vmcnt(0)", "s_barrier", "s_nop 7", "s_nop 7"]
+    if VARIANT["ks"]:
+        body += ["s_cmp_gt_u32 %[kss], 1", "s_cbranch_scc1 L_ks_%="]
     body += ["s_bitcmp1_b32 %[flags], 0", "s_cbranch_scc1 L_collect_%="]
     if VARIANT["bar2"] or VARIANT["il"]:
         # (with bar2 / il: the plain epilogue stores each 16-row batch as
@@ -1028,6 +1159,11 @@ def _build(dt, wave_epi, last_block, stamps):
     body.append("L_got_%=:")
     body += epilogue_body(cvt, "collect", wave_epi)
     body.append("s_branch L_done_%=")
+    if VARIANT["ks"]:
+        body += ksplit()
+        for S in KS_CHUNKS:
+            for g in range(S):
+                body += ksplit_path(cvt, S, g, stamps)
     body.append("L_nan_%=:")
     body += epilogue_body(cvt, "nan", wave_epi)
     body += ["L_done_%=:"]
@@ -1061,13 +1197,20 @@ def render():
                                            ("_W2_SDD", False, True, True, False, False),
                                            ("_W2_SDD_NT", False, True, True, True, False),
                                            ("_W2_SDD_TT", False, True, True, False, True),
+                                           ("_W2_SDD_KS", False, True, True, False, False),
                                            ("_W2_NT", False, True, False, True, False),
                                            ("_W2_DDS_NT", True, True, False, True, False),
                                            ("_W2_TT", False, True, False, False, True)):
             lines.append(f"#define DSD4W_ASM_{dt.upper()}{name} \\")
             lines += [f'  "{ins}\\n" \\'
-                      for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt)]
+                      for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt,
+                                       ks=name.endswith("_KS"))]
             lines += ['  ""', ""]
+        # the SDD K-split with timeline stamps (experiment builds)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_SDD_KS_T \\")
+        lines += [f'  "{ins}\\n" \\'
+                  for ins in build(dt, True, False, True, ds=True, sdd=True, ks=True)]
+        lines += ['  ""', ""]
         # DSD / DDS / SDD TN (per-step images, per-wave epilogue)
         for name, dds, sdd in (("_W_TN", False, False), ("_W_DDS_TN", True, False),
                                ("_W_SDD_TN", False, True)):

@@ -304,6 +304,166 @@ def test_kat_sdd_grouped(ta, tb, k):
     _equal(got, want, f"sdd grouped {ta}{tb} k={k}")
 
 
+# (m, k, n, stored blocks, dtype): one CU's workgroup per chunk, S picked
+# in-kernel from the group count (dsd4w.hip kKs): 8 rows x 60 blocks with
+# K = 2048 -> S = 8 (2 k-blocks per chunk, many partial groups); 150 blocks,
+# K = 1152 (9 k-blocks: chunks of 2, 2, 2, 3) -> S = 4; 300 blocks, K = 512
+# -> S = 2; config 3's shape (205 blocks of 4096^2, K = 4096) -> S = 4.
+KSPLIT_CASES = [
+    (1024, 2048, 4096, 60, "f16"),
+    (1024, 2048, 4096, 60, "bf16"),
+    (4096, 1152, 4096, 150, "f16"),
+    (4096, 512, 4096, 300, "f16"),
+    (4096, 4096, 4096, 205, "bf16"),
+]
+
+
+@pytest.fixture
+def ksplit_any_k():
+    """The K-split for every K >= 512 (default: K >= 6144, knob
+    sdd_ksplit_min_k), so these small problems take it."""
+    prev = sp.tuning("sdd_ksplit_min_k", 512)
+    yield
+    sp.tuning("sdd_ksplit_min_k", prev)
+
+
+@pytest.mark.parametrize("m,k,n,nb,dtype", KSPLIT_CASES)
+def test_kat_sdd_ksplit(m, k, n, nb, dtype, ksplit_any_k):
+    """SDD NN below the grouped threshold with few groups: each group's K
+    split over 2-8 workgroups whose fp32 partials are summed by the chunk
+    that owns each row slice (dsd4w.hip kKs, gen_dsd4w.py ksplit_path).
+    Exact integer operands: every order of the fp32 sums is exact, so the
+    result equals the float64 product bit for bit; a second launch on the
+    and no chunk timed out."""
+    got, want, plan = kat_sdd(m, k, n, None, False, False, dtype, nb=nb,
+                              seed=nb + k)
+    assert plan == 2, "K-split SDD not selected"
+    _equal(got, want, f"sdd ksplit {m}x{k}x{n} nb={nb} {dtype}")
+    assert sp.pair_errors() == 0
+
+
+def test_sdd_ksplit_deterministic_and_close(ksplit_any_k):
+    """Random (non-integer) operands at config 3's shape: the K-split sum
+    order is fixed (each chunk adds the others' partials in chunk order after
+    its own), so two launches are bit-identical; the result is within the
+    north-star tolerance of the 8-wave k-split kernel (knob sdd_ksplit = 1)
+    and of the oracle on 24 blocks."""
+    rng = np.random.default_rng(33)
+    d, nb = 4096, 205
+    off, idx = mu.random_topology(d // B, d // B, nb, rng)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(33)
+    x = (torch.rand(d * d, generator=g, device="cuda") * 2 - 1).half()
+    w = (torch.rand(d * d, generator=g, device="cuda") * 2 - 1).half()
+    cv = torch.empty(nb * B * B, dtype=torch.float16, device="cuda")
+    Cm = sp.BlockMatrix(d, d, B, nb * B * B, cv,
+                        torch.from_numpy(off.astype(np.int32)).cuda(),
+                        torch.from_numpy(idx.astype(np.int16)).cuda())
+    sp.AllocateRowIndicesBuffer(Cm)
+    sp.RowIndices(Cm, Cm.row_indices)
+    X, W = sp.Matrix(d, d, x), sp.Matrix(d, d, w)
+    assert sp.sdd_plan(X, False, W, False, Cm) == 2
+
+    def run():
+        cv.fill_(float("nan"))
+        sp.Matmul(X, False, W, False, Cm)
+        torch.cuda.synchronize()
+        return cv.clone()
+    a, b = run(), run()
+    assert torch.equal(a, b), "K-split SDD not deterministic"
+    prev = sp.tuning("sdd_ksplit", 1)
+    try:
+        assert sp.sdd_plan(X, False, W, False, Cm) == 0
+        ref8 = run()
+    finally:
+        sp.tuning("sdd_ksplit", prev)
+    diff = (a.float() - ref8.float()).abs().max().item()
+    assert diff <= 1e-2 * ref8.float().abs().max().item(), diff
+    from oracle import oracle as O
+    from tests import helpers
+    xv = x.float().cpu().numpy().reshape(d, d)
+    wv = w.float().cpu().numpy().reshape(d, d)
+    rows = np.repeat(np.arange(d // B), np.diff(off))
+    got = a.view(-1, B, B).float().cpu().numpy()
+    for e in sorted(set([0, nb - 1] + [int(v) for v in rng.choice(nb, 22, replace=False)])):
+        r, c = int(rows[e]), int(idx[e])
+        ref = O.gemm(np.ascontiguousarray(xv[r * B:(r + 1) * B]), False,
+                     np.ascontiguousarray(wv[:, c * B:(c + 1) * B]), False)
+        helpers.assert_close(got[e], ref, "f16", f"sdd ksplit block {e}")
+    assert sp.pair_errors() == 0
+
+
+def test_sdd_ksplit_timeout_fails_loudly(ksplit_any_k):
+    """With the test fault on, no chunk raises its flag: every chunk times
+    out after the bounded wait, its rows become NaN, the time-outs are
+    counted, and the next launch is exact again (per-launch epochs)."""
+    got, want, plan = kat_sdd(1024, 2048, 4096, None, False, False, "f16", nb=60,
+                              seed=3)
+    assert plan == 2
+    _equal(got, want, "before fault")
+    rng = np.random.default_rng(3)
+    A = IDense(1024, 2048, rng, "f16")
+    Bd = IDense(2048, 4096, rng, "f16")
+    Cs = ISparse(1024, 4096, None, rng, "f16", nb=60)
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    want2 = _expect(Cs.blocks_of(A.values.astype(np.float64) @ Bd.values), "f16")
+    sp.lib().sputnik_debug_pair_fault(1)
+    try:
+        Cs.dev.fill_(0)
+        sp.Matmul(A.m, False, Bd.m, False, Cs.m)
+        torch.cuda.synchronize()
+    finally:
+        sp.lib().sputnik_debug_pair_fault(0)
+    assert bool(torch.isnan(Cs.dev.float()).all()), "timed-out chunks not NaN"
+    assert sp.pair_errors() > 0
+    Cs.dev.fill_(float("nan"))
+    sp.Matmul(A.m, False, Bd.m, False, Cs.m)
+    _equal(Cs.dev, want2, "after fault")
+    assert sp.pair_errors() == 0
+
+
+def test_graph_capture_sdd_ksplit(ksplit_any_k):
+    """A K-split SDD captured into a graph: replays (back to back and with
+    eager launches in between) read the device-side epoch and stay exact."""
+    rng = np.random.default_rng(8)
+    A = IDense(4096, 4096, rng, "f16")
+    Bd = IDense(4096, 4096, rng, "f16")
+    Cs = ISparse(4096, 4096, None, rng, "f16", nb=205)
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    want = _expect(Cs.blocks_of(A.values.astype(np.float64) @ Bd.values), "f16")
+    assert sp.sdd_plan(A.m, False, Bd.m, False, Cs.m) == 2
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.Matmul(A.m, False, Bd.m, False, Cs.m)
+    for i in range(3):
+        Cs.dev.fill_(float("nan"))
+        g.replay()
+        _equal(Cs.dev, want, f"replay {i}")
+        Cs.dev.fill_(float("nan"))
+        sp.Matmul(A.m, False, Bd.m, False, Cs.m)
+        _equal(Cs.dev, want, f"eager {i}")
+    for _ in range(6):
+        g.replay()
+    _equal(Cs.dev, want, "back-to-back replays")
+    assert sp.pair_errors() == 0
+    del g
+
+
+def test_sdd_plan_ksplit_default_gate():
+    """Default gate: 205 blocks of 4096^2 take the 8-wave k-split tile at
+    K = 4096 and the K-split grouped tiles at K = 8192 (exact there too)."""
+    for k, want in ((4096, 0), (8192, 2)):
+        got, exp, plan = kat_sdd(4096, k, 4096, None, False, False, "f16", nb=205,
+                                 seed=k)
+        assert plan == want, (k, plan)
+        _equal(got, exp, f"sdd 205 blocks k={k}")
+    assert sp.pair_errors() == 0
+
+
 def test_sdd_plan_threshold():
     """Just below 5 blocks per CU the k-split block tile is chosen, from 5
     the grouped one (dispatch.cpp UseGroupedSdd)."""
