@@ -1206,6 +1206,11 @@ def render():
                       for ins in build(dt, True, False, False, dds, ds, sdd, nt, tt,
                                        ks=name.endswith("_KS"))]
             lines += ['  ""', ""]
+        # DDS NN (double slots) with timeline stamps (experiment builds)
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_DDS_T \\")
+        lines += [f'  "{ins}\\n" \\'
+                  for ins in build(dt, True, False, True, dds=True, ds=True)]
+        lines += ['  ""', ""]
         # the SDD K-split with timeline stamps (experiment builds)
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_SDD_KS_T \\")
         lines += [f'  "{ins}\\n" \\'

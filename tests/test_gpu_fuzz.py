@@ -6,7 +6,8 @@ setup code branches on (VERDICT r04 "what's weak" 1): odd and even block
 counts, a last block-row of 0, 1 or 2 blocks (with an odd count the last
 entry shares its dword of the index list), 1023 / 1024 / 1025 stored blocks
 (around the 1024-entry index preload, dsd4w.hip kIdxPreload), an index list
-whose pointer is 2 bytes off 16-byte alignment (the scalar-load fallback),
+whose pointer is 2 bytes off 16-byte alignment and a transposed block-offset
+list 4 bytes off (the scalar-load fallbacks),
 heavy/light/empty rows (pair hand-offs), 8 / 16 / 32 block-rows (split mode,
 pairs), and pair balancing on and off (tuning knob "pairs"). Then:
 
@@ -131,6 +132,15 @@ def dev_index(idx, unaligned):
     return t
 
 
+def dev_offsets(nb):
+    """int32 block-offset list (filled by Transpose) 4 bytes past a 16-byte
+    boundary: the 4-wave kernel's block-offset preload falls back to scalar
+    loads."""
+    t = torch.empty(nb + 1, dtype=torch.int32, device="cuda")[1:]
+    assert t.data_ptr() % 16 == 4
+    return t
+
+
 def rnd(n, g, td):
     return (torch.rand(max(n, 1), generator=g, device="cuda") * 2 - 1).to(td)
 
@@ -225,6 +235,7 @@ def test_fuzz_dsd(kind, R, KB, N, unaligned, trans, pairs):
         sp.AllocateTransposeBuffers(A)
         if unaligned:  # A^T's index list (the one the kernel reads) off by 2
             A.indices_t = dev_index(np.zeros(nb, np.int16), True)
+            A.block_offsets = dev_offsets(nb)
         sp.Transpose(A)
     Bm = sp.Matrix(N, K, b) if tb else sp.Matrix(K, N, b)
 
@@ -292,6 +303,7 @@ def test_fuzz_dds(kind, R, KB, M, unaligned, trans, pairs):
         sp.AllocateTransposeBuffers(Bs)
         if unaligned:
             Bs.indices_t = dev_index(np.zeros(nb, np.int16), True)
+            Bs.block_offsets = dev_offsets(nb)
         sp.Transpose(Bs)
     Am = sp.Matrix(K, M, a) if ta else sp.Matrix(M, K, a)
 
