@@ -166,7 +166,8 @@ int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
 /* DSD kernel plan of a problem launched on `stream` (no launch; makes the
  * launch's workspace decisions): 0 = the 8-wave 128x512 tile, 1 = the
  * 4-wave hand-scheduled kernel, 2 = the tall configuration, 3 = split mode,
- * -1 = the problem is rejected. */
+ * 4 = the tall pipeline (4-wave, persistent, NN), -1 = the problem is
+ * rejected. */
 int sputnik_dsd_plan(const sputnik_block_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_matrix_t *c, hipStream_t stream);

@@ -420,7 +420,8 @@ def can_implement(op: str, a, transpose_a, b, transpose_b, c) -> bool:
 
 def dsd_plan(a, transpose_a, b, transpose_b, c, stream=None) -> int:
     """Kernel a DSD launch on `stream` (torch's current stream by default)
-    would use: 0 8-wave tile, 1 4-wave kernel, 2 tall, 3 split, -1 rejected
+    would use: 0 8-wave tile, 1 4-wave kernel, 2 tall, 3 split, 4 tall
+    pipeline (4-wave, persistent), -1 rejected
     (sputnik_dsd_plan)."""
     if stream is None:
         import torch

@@ -53,7 +53,7 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 // the current device (no launch).
 int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
 // DSD kernel plan (dispatch.cpp DsdPlan): 0 8-wave tile, 1 4-wave kernel,
-// 2 tall, 3 split mode, -1 rejected.
+// 2 tall, 3 split mode, 4 tall pipeline, -1 rejected.
 int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
             hipStream_t stream);
 
@@ -90,6 +90,7 @@ enum KnobId {
   kKnobSddKsplit,
   kKnobSddKsplitMinK,
   kKnobSddOrder,
+  kKnobTall4w,
   kNumKnobs
 };
 int Knob(KnobId k);

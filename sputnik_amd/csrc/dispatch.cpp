@@ -114,6 +114,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
     {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
+    {"tall4w", "SPUTNIK_AMD_TALL4W", 0, 0, 1},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1016,6 +1017,33 @@ bool UseTall(GemmParams *p, hipStream_t stream, bool dry = false) {
 
 // ---- shared entry points -------------------------------------------------
 
+// Tall DSD NN on the 4-wave kernel, persistent (dsd4w.hip kEpi 7): one
+// workgroup per CU walks a cost-balanced contiguous range of the
+// panel-major block sequence (512-column panels) and stores each 128 x 512
+// tile through a free ring slot as soon as its last block is done, the next
+// tile's first DMAs in flight meanwhile; the empty rows' tiles are
+// zero-filled after, an equal share per workgroup. Needs whole 512-column
+// panels, at most 128 blocks and 64 zero chunks per workgroup, and rows that
+// fit the LDS copy of the offsets.
+static bool UseTallPipe(const GemmParams &p, long long blocks, long long row_max, bool ta,
+                        bool tb) {
+  if (Knob(kKnobTall4w) == 0 || !Dsd4wEnabled() || ta || tb) return false;
+  if (p.pair != 0 || p.pair_split > 1 || CfgSparse::kBN != 512) return false;
+  if (p.j_limit % 512 != 0 || p.num_rows > 32767 || blocks <= 0) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  const int cus = DeviceCUs(dev);
+  if (cus <= 0) return false;
+  // blocks per workgroup: a weighted share (a tile weighs its blocks + 1:
+  // blocks + non-empty rows per panel) plus the tile the cut runs into
+  const long long per =
+      ((blocks + std::min<long long>(blocks, p.num_rows)) * (p.j_limit / 512) + cus - 1) / cus;
+  // (the empty rows' zero chunks: an equal share of at most panels x rows)
+  const long long zero_per = ((long long)(p.j_limit / 512) * p.num_rows + cus - 1) / cus;
+  return per + row_max <= 128 && zero_per <= 64 && blocks < (1LL << 24) &&
+         p.j_limit / 512 < 256;
+}
+
 hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
                   const Matrix &c, int dtype, bool build_meta,
                   hipStream_t stream, Status *st_out) {
@@ -1030,7 +1058,17 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   }
   p.debug = g_debug;
   PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
+  const GemmParams p0 = p;  // (before the tall configuration)
   const bool tall = UseTall(&p, stream);
+  if (tall && UseTallPipe(p0, a.nonzeros / (kBlock * kBlock),
+                          ((long long)a.cols + kBlock - 1) / kBlock, ta, tb)) {
+    GemmParams q = p0;
+    q.persistent = 0;
+    q.num_jtiles = q.j_limit / 512;
+    int dev = 0;
+    q.num_tiles = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
+    return LaunchDsd4w(dtype, q, 7, false, stream, false, false);
+  }
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall)) {
@@ -1364,7 +1402,8 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
 
 // Which kernel RunDsd would launch for this problem on `stream` (no
 // launch): 0 the 8-wave 128 x 512 tile, 1 the 4-wave hand-scheduled kernel
-// (dsd4w.hip), 2 the tall configuration, 3 split mode, -1 rejected. Read-only:
+// (dsd4w.hip), 2 the tall configuration, 3 split mode, 4 the tall
+// pipeline (4-wave, persistent), -1 rejected. Read-only:
 // it makes the workspace decisions a launch would make without allocating,
 // re-tying or advancing any workspace (safe during a capture).
 int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
@@ -1377,7 +1416,11 @@ int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
                  *static_cast<const Matrix *>(c), &p, &needs_meta) != Status::kOk)
     return -1;
   PreparePairs(&p, am.nonzeros / (kBlock * kBlock), stream, /*dry=*/true);
+  const GemmParams p0 = p;
   const bool tall = UseTall(&p, stream, /*dry=*/true);
+  if (tall && UseTallPipe(p0, am.nonzeros / (kBlock * kBlock),
+                          ((long long)am.cols + kBlock - 1) / kBlock, ta, tb))
+    return 4;
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : am.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall))

@@ -124,8 +124,14 @@ def dmas(slot):
 # [32 k][128 n] slice (8 KiB contiguous: S advances 32 rows of 256 B) and
 # the wave's image [128 m][32 k] of the dense rows (D advances 64 B).
 VARIANT = {"dds": False, "ds": False, "sdd": False, "nt": False, "tt": False,
-           "bar2": False, "tn": False, "ddstt": False, "il": False, "ks": False}
+           "bar2": False, "tn": False, "ddstt": False, "il": False, "ks": False,
+           "tp": False}
 # "ks": SDD K-split (ksplit_path): the epilogue of a chunk of a group's K.
+# "tp": tall DSD NN, persistent (tall_flush): a workgroup's blocks come from
+# per-lane tables (%[vent]: lane x = CSR entry | panel << 24 of virtual block
+# x, %[vent2] of block 64 + x; %[vtile] / %[vtile2]: row | panel << 16 |
+# last-of-tile << 31) and every tile is stored as soon as its last block is
+# done.
 # "il": the plain per-wave epilogue stores each 16-row batch as soon as it is
 # staged (on with "bar2"; alone: _W4).
 # DDS TT ("ddstt", with "ds"): B's rows (storage order) are the shared image
@@ -188,7 +194,15 @@ def advance():
 
 
 def entry_of(xreg, out_reg):
-    """out_reg = absolute CSR entry of virtual entry xreg (scc clobbered)."""
+    """out_reg = absolute CSR entry of virtual entry xreg (scc clobbered).
+    (tp: lane xreg of %[vent]; the lane select written by SALU just before
+    needs 4 wait states.)"""
+    if VARIANT["tp"]:  # (128 entries: lanes of %[vent] then of %[vent2])
+        tmp = "s77" if out_reg == "s76" else "s76"
+        return ["s_nop 3", f"v_readlane_b32 {out_reg}, %[vent], {xreg}",
+                f"v_readlane_b32 {tmp}, %[vent2], {xreg}", f"s_cmp_lt_u32 {xreg}, 64",
+                f"s_cselect_b32 {out_reg}, {out_reg}, {tmp}",
+                f"s_and_b32 {out_reg}, {out_reg}, 0xffffff"]
     return [f"s_cmp_lt_u32 {xreg}, %[n1]",
             f"s_cselect_b32 {out_reg}, %[b1], %[b2m]",
             f"s_add_u32 {out_reg}, {out_reg}, {xreg}"]
@@ -214,8 +228,14 @@ def switch():
                + [f"s_lshr_b32 s77, s76, {hi}", f"s_lshl_b32 s76, s76, {lo}"])
     out = blk + ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
                  "s_mul_i32 s76, s58, %[k128]", "s_mul_hi_u32 s77, s58, %[k128]",
-                 "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77",
-                 "s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"]
+                 "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
+    if VARIANT["tp"]:  # + the block's panel: 512 columns = 1 KiB
+        out += ["v_readlane_b32 s79, %[vent], s57", "v_readlane_b32 s78, %[vent2], s57",
+                "s_cmp_lt_u32 s57, 64", "s_cselect_b32 s79, s79, s78",
+                "s_lshr_b32 s79, s79, 24",
+                "s_lshl_b32 s79, s79, 10", "s_add_u32 s44, s44, s79",
+                "s_addc_u32 s45, s45, 0"]
+    out += ["s_lshr_b32 s58, s59, s60", "s_and_b32 s58, s58, 0xffff"]
     if col_order():
         out.append("s_mov_b32 s63, s62")
     return out
@@ -753,6 +773,10 @@ def prologue_setup():
     out += ["s_add_u32 s40, %[sdlo], s76", "s_addc_u32 s41, %[sdhi], s77",
             "s_mul_i32 s76, %[kb0], %[k128]", "s_mul_hi_u32 s77, %[kb0], %[k128]",
             "s_add_u32 s44, %[dtlo], s76", "s_addc_u32 s45, %[dthi], s77"]
+    if VARIANT["tp"]:
+        out += ["v_readlane_b32 s79, %[vent], 0", "s_lshr_b32 s79, s79, 24",
+                "s_lshl_b32 s79, s79, 10", "s_add_u32 s44, s44, s79",
+                "s_addc_u32 s45, s45, 0"]
     return out
 
 
@@ -908,6 +932,74 @@ def poll():
             "s_branch L_nan_%="]
 
 
+TP_NO_STORES = [False]  # (experiment variant _W2_TP_NS: the flush without its stores)
+
+
+def tall_flush(cvt, dt):
+    """tp: the tile of the block just finished (%[vtile] lane s74 in s75:
+    row, panel) is complete. Its 128 x 128 block per wave goes out through
+    the one ring slot free at this point -- per-step slot 3 of the wave's D
+    ring (8 KiB at 24 KiB: step 3's data, read during step 2; the next
+    block's steps 0-2 are in flight into slots 0-2, step 3's DMA is issued in
+    its step 0) -- in four rounds of 32 rows: accumulators -> fp16 / bf16 ->
+    the per-wave staging layout (epilogue_body), then read back as 4 rows x
+    256 B per store (copy_out). Fragment set 1 (v[192:255]: step 3's, done;
+    step 0 reads step 1's into it only after this) holds the read-back
+    rows. Then drain and restart the next tile's first block from zero (or
+    end)."""
+    out = ["L_tflush_%=:", "s_nop 7", "s_nop 7", "s_nop 7",
+           "s_and_b32 s76, s75, 0xffff",
+           "s_mul_i32 s84, s76, %[crow]", "s_mul_hi_u32 s85, s76, %[crow]",
+           "s_add_u32 s84, s84, %[cdlo]", "s_addc_u32 s85, s85, %[cdhi]",
+           "s_lshr_b32 s77, s75, 16", "s_and_b32 s77, s77, 0xff",
+           "s_lshl_b32 s77, s77, 10",
+           "s_add_u32 s84, s84, s77", "s_addc_u32 s85, s85, 0",
+           "s_mov_b32 s86, 0x7fffffff", "s_mov_b32 s87, 0x00020000"]
+    win = 3 * SLOT
+    for k in range(4):
+        for m in (2 * k, 2 * k + 1):
+            for n in range(8):
+                i = 8 * m + n
+                t = 96 + 8 * (i % 4)
+                out += [f"v_accvgpr_read_b32 v{t + j}, a{4 * i + j}" for j in range(4)]
+                out += [f"{cvt} v{t + 4}, v{t}, v{t + 1}", f"{cvt} v{t + 5}, v{t + 2}, v{t + 3}",
+                        f"ds_write_b64 %[vws{n}], v[{t + 4}:{t + 5}] "
+                        f"offset:{win + 4096 * (m - 2 * k)}"]
+        out += ["s_waitcnt lgkmcnt(0)", f"s_mul_i32 s78, %[c4], {8 * k}"]
+        for b in (2 * k, 2 * k + 1):
+            base = 192 + 16 * (b % 2)
+            for j in range(4):
+                out.append(f"ds_read_b128 v[{base + 4 * j}:{base + 4 * j + 3}], "
+                           f"%[vrb{j}] offset:{win + 4096 * (b - 2 * k)}")
+            out.append("s_waitcnt lgkmcnt(0)")
+            if TP_NO_STORES[0]:
+                continue
+            for j in range(4):
+                out += [f"buffer_store_dwordx4 v[{base + 4 * j}:{base + 4 * j + 3}], %[vco], "
+                        f"s[84:87], s78 offen nt",
+                        "s_add_u32 s78, s78, %[c4]"]
+    # The next block's steps 0 and 1 run with their waits recounted over
+    # the instruction stream (as publish_sequence): the DMAs they wait for
+    # are older than these stores, which may still fly; step 2 waits for
+    # step 0's DMAs, younger than the stores, with the loop's own count.
+    out += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_fin_%="]
+    ctx = [step_ds(dt, 2), step_ds(dt, 3) + out]
+
+    def younger_than_dma_of(t, steps):
+        dm = [k for k, x in enumerate(steps[t]) if x.startswith("buffer_load")
+              and x.endswith("lds")]
+        ops = [x for x in steps[t][dm[-1] + 1:] if _is_vmem(x)]
+        for u in range(t + 1, len(steps)):
+            ops += [x for x in steps[u] if _is_vmem(x)]
+        return len(ops)
+    w0 = younger_than_dma_of(0, ctx)
+    s0 = step_ds(dt, 0, zero_c=True, wait=w0)
+    w1 = younger_than_dma_of(1, ctx + [s0])
+    s1 = step_ds(dt, 1, wait=w1)
+    assert w0 <= 63 and w1 <= 63, (w0, w1)
+    return out + s0 + s1 + ["s_branch L_s2_%="]
+
+
 KS_CHUNKS = (2, 4, 8)
 
 
@@ -1037,14 +1129,14 @@ def ksplit():
 
 def build(dt, wave_epi=False, last_block=False, stamps=False, dds=False, ds=False,
           sdd=False, nt=False, tt=False, bar2=False, tn=False, ddstt=False, il=False,
-          ks=False):
+          ks=False, tp=False):
     VARIANT.update(dds=dds, ds=ds, sdd=sdd, nt=nt, tt=tt, bar2=bar2, tn=tn, ddstt=ddstt,
-                   il=il, ks=ks)
+                   il=il, ks=ks, tp=tp)
     try:
         return _build(dt, wave_epi, last_block, stamps)
     finally:
         VARIANT.update(dds=False, ds=False, sdd=False, nt=False, tt=False, bar2=False,
-                       tn=False, ddstt=False, il=False, ks=False)
+                       tn=False, ddstt=False, il=False, ks=False, tp=False)
 
 
 def _build(dt, wave_epi, last_block, stamps):
@@ -1071,8 +1163,13 @@ def _build(dt, wave_epi, last_block, stamps):
                          "s_cmp_eq_u32 s61, %[publast]", "s_cbranch_scc1 L_publ_%="]
             body.append("L_s3_%=:")
         body += step(dt, H)
-    body += ["s_sub_u32 s61, s61, 1",
-             "s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%="]
+    body.append("s_sub_u32 s61, s61, 1")
+    if VARIANT["tp"]:  # the block just done ends its tile: store the tile
+        body += ["s_sub_u32 s74, %[ntot], s61", "s_sub_u32 s74, s74, 1", "s_nop 3",
+                 "v_readlane_b32 s75, %[vtile], s74", "v_readlane_b32 s76, %[vtile2], s74",
+                 "s_cmp_lt_u32 s74, 64", "s_cselect_b32 s75, s75, s76",
+                 "s_bitcmp1_b32 s75, 31", "s_cbranch_scc1 L_tflush_%="]
+    body += ["s_cmp_eq_u32 s61, %[flushrem]", "s_cbranch_scc1 L_pub_%="]
     if early:  # pair consumer: flag load / consumer last block
         body += ["s_cmp_eq_u32 s61, %[clbf]", "s_cbranch_scc1 L_clbf_%=",
                  "s_cmp_eq_u32 s61, %[clbc]", "s_cbranch_scc1 L_clbc_%="]
@@ -1159,6 +1256,8 @@ def _build(dt, wave_epi, last_block, stamps):
     body.append("L_got_%=:")
     body += epilogue_body(cvt, "collect", wave_epi)
     body.append("s_branch L_done_%=")
+    if VARIANT["tp"]:
+        body += tall_flush(cvt, dt)
     if VARIANT["ks"]:
         body += ksplit()
         for S in KS_CHUNKS:
@@ -1210,6 +1309,20 @@ def render():
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_DDS_T \\")
         lines += [f'  "{ins}\\n" \\'
                   for ins in build(dt, True, False, True, dds=True, ds=True)]
+        lines += ['  ""', ""]
+        # tall DSD NN, persistent (tall_flush), with and without stamps
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_TP \\")
+        lines += [f'  "{ins}\\n" \\' for ins in build(dt, True, ds=True, tp=True)]
+        lines += ['  ""', ""]
+        TP_NO_STORES[0] = True
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_TP_NS \\")
+        lines += [f'  "{ins}\\n" \\'
+                  for ins in build(dt, True, False, True, ds=True, tp=True)]
+        lines += ['  ""', ""]
+        TP_NO_STORES[0] = False
+        lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_TP_T \\")
+        lines += [f'  "{ins}\\n" \\'
+                  for ins in build(dt, True, False, True, ds=True, tp=True)]
         lines += ['  ""', ""]
         # the SDD K-split with timeline stamps (experiment builds)
         lines.append(f"#define DSD4W_ASM_{dt.upper()}_W2_SDD_KS_T \\")

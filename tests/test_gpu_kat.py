@@ -161,6 +161,44 @@ def test_kat_tall_persistent_repeated():
         _equal(c_t, want, f"tall persistent launch {i}")
 
 
+# Tall DSD NN on the persistent 4-wave pipeline (dsd4w.hip kEpi 7, plan 4):
+# (m, k, n, density, dtype). 300 block-rows x 4 k-blocks, two 512 panels;
+# a near-empty operand whose workgroup ranges are 0-1 blocks and cross
+# panel boundaries (bf16); rows of up to 16 blocks over one panel; a full
+# operand of 32-block rows whose workgroup ranges pass 64 blocks (the second
+# lane tables, %[vent2] / %[vtile2]).
+TALL_PIPE_CASES = [
+    (300 * 128, 512, 1024, 0.05, "f16"),
+    (300 * 128, 256, 2048, 0.02, "bf16"),
+    (300 * 128, 2048, 512, 0.02, "f16"),
+    (280 * 128, 4096, 1024, 1.0, "f16"),
+]
+
+
+@pytest.fixture
+def tall_pipe():
+    prev = sp.tuning("tall4w", 1)
+    yield
+    sp.tuning("tall4w", prev)
+
+
+@pytest.mark.parametrize("m,k,n,density,dtype", TALL_PIPE_CASES)
+def test_kat_dsd_tall_pipe(m, k, n, density, dtype, tall_pipe):
+    """Every tile of a tall DSD NN from the persistent 4-wave pipeline:
+    stored straight from the accumulators at the tile's last block, empty
+    rows zero-filled after; exact against the float64 product, run twice
+    (stale output from the first launch would show on a NaN-filled C)."""
+    rng = np.random.default_rng(int(density * 1000) + k)
+    A = ISparse(m, k, density, rng, dtype)
+    Bd = IDense(k, n, rng, dtype)
+    want = _expect(A.dense.astype(np.float64) @ Bd.values, dtype)
+    for rep in range(2):
+        C, c_t = _nan_out(m, n, dtype)
+        assert sp.dsd_plan(A.m, False, Bd.m, False, C) == 4
+        sp.Matmul(A.m, False, Bd.m, False, C)
+        _equal(c_t, want, f"tall pipe {m}x{k}x{n} {density} {dtype} rep {rep}")
+
+
 @pytest.mark.parametrize("ta", [False, True])
 def test_kat_dsd_4096_pairs(ta):
     """BASELINE config 2 shape (4096^3, 50%): one tile per CU, the
