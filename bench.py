@@ -175,6 +175,32 @@ def pmc_traffic(path, key, build_hash):
     return entry.get("hbm_bytes_per_launch"), "rocprofv3 --pmc, same build"
 
 
+PEAK_CLOCK_GHZ = 2.4  # MI355X peak engine clock (the 2.5 PF dense fp16 figure)
+
+
+def pmc_clock(path, key, build_hash, achieved_tflops, peak_tflops):
+    """The clock and matrix-pipe busy fraction PMC measured for this exact
+    build (scripts/pmc.sh), and `achieved` against the matrix peak at that
+    clock (peak x clock / 2.4 GHz): the chip does not hold its peak clock
+    under this load, so `frac` alone understates how full the pipe is."""
+    try:
+        with open(path) as f:
+            entry = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+    if not entry or entry.get("build_hash") != build_hash:
+        return None
+    ghz = entry.get("est_clock_GHz")
+    if not ghz:
+        return None
+    peak_at = peak_tflops * ghz / PEAK_CLOCK_GHZ
+    return {"clock_GHz": ghz, "mfma_busy_frac": entry.get("mfma_busy_frac"),
+            "profiled_kernel_us": entry.get("profiled_kernel_us"),
+            "peak_at_clock": round(peak_at, 1),
+            "frac_at_clock": round(achieved_tflops / peak_at, 4),
+            "source": "rocprofv3 --pmc (profiles/pmc_latest.json), same build"}
+
+
 # --------------------------------------------------------------- problems --
 
 def _values(n, td, gen, device):
@@ -231,6 +257,8 @@ class DsdProblem:
                f"hand-scheduled k-loop>",
             2: f"block_gemm_kernel<{dtype}, {tr}, tall 128x256 x2 per CU>",
             3: f"block_gemm_kernel<{dtype}, {tr}, split mode>",
+            4: f"dsd4w_kernel<{dtype}, {tr}, tall pipeline: 4 waves, one workgroup "
+               f"per CU, 128x512 tiles stored at their last block>",
         }.get(plan, f"block_gemm_kernel<{dtype}, {tr}, 128x512 staggered tile>")
 
     def launcher(self):
@@ -853,6 +881,10 @@ def main():
         roof = roofline(prob.flops, prob.bytes, per_step * 1e-3, prob.kernel,
                         traffic)
         roof["traffic_source"] = note
+        if roof.get("bound") == "mfma":
+            pc = pmc_clock(args.pmc, key, build.get("hash"), tflops, roof["peak"])
+            if pc is not None:
+                roof["pmc_clock"] = pc
         results[d] = {"value": round(tflops, 2), "ms_per_step": round(per_step, 5),
                       "nnz_blocks_per_rank": prob.nb, "roofline": roof}
         if head is None:

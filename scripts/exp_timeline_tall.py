@@ -40,6 +40,8 @@ def main():
            "compute": stats(us(t[has, 4] - t[has, 2])),
            "per_block": stats(us(t[has, 4] - t[has, 2]) / np.maximum(t[has, 5], 1)),
            "compute_end": stats(us(t[has, 4] - e0)),
+           "flush_sum": stats(us(t[has, 9] & 0xffffffff)),
+           "after_flush_2steps_sum": stats(us(t[has, 9] >> 32)),
            "zero_fill": stats(us(t[:, 15] - np.where(t[:, 4] > 0, t[:, 4], t[:, 0]))),
            "end": stats(us(t[:, 15] - e0))}
     print(json.dumps(out), flush=True)

@@ -114,7 +114,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
     {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
-    {"tall4w", "SPUTNIK_AMD_TALL4W", 0, 0, 1},
+    {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];

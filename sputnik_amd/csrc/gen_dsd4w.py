@@ -935,7 +935,7 @@ def poll():
 TP_NO_STORES = [False]  # (experiment variant _W2_TP_NS: the flush without its stores)
 
 
-def tall_flush(cvt, dt):
+def tall_flush(cvt, dt, stamps=False):
     """tp: the tile of the block just finished (%[vtile] lane s74 in s75:
     row, panel) is complete. Its 128 x 128 block per wave goes out through
     the one ring slot free at this point -- per-step slot 3 of the wave's D
@@ -947,7 +947,10 @@ def tall_flush(cvt, dt):
     step 0 reads step 1's into it only after this) holds the read-back
     rows. Then drain and restart the next tile's first block from zero (or
     end)."""
-    out = ["L_tflush_%=:", "s_nop 7", "s_nop 7", "s_nop 7",
+    out = ["L_tflush_%=:"]
+    if stamps:  # (timeline: %[r3] += flush time, %[r4] += the next two steps')
+        out += ["s_memrealtime s[96:97]", "s_waitcnt lgkmcnt(0)"]
+    out += ["s_nop 7", "s_nop 7", "s_nop 7",
            "s_and_b32 s76, s75, 0xffff",
            "s_mul_i32 s84, s76, %[crow]", "s_mul_hi_u32 s85, s76, %[crow]",
            "s_add_u32 s84, s84, %[cdlo]", "s_addc_u32 s85, s85, %[cdhi]",
@@ -982,6 +985,10 @@ def tall_flush(cvt, dt):
     # the instruction stream (as publish_sequence): the DMAs they wait for
     # are older than these stores, which may still fly; step 2 waits for
     # step 0's DMAs, younger than the stores, with the loop's own count.
+    if stamps:  # s88 += this flush, s89 += the next two steps (s96: their start)
+        out += ["s_memrealtime s[98:99]", "s_waitcnt lgkmcnt(0)",
+                "s_sub_u32 s96, s98, s96", "s_add_u32 s88, s88, s96",
+                "s_mov_b32 s96, s98"]
     out += ["s_cmp_eq_u32 s61, 0", "s_cbranch_scc1 L_fin_%="]
     ctx = [step_ds(dt, 2), step_ds(dt, 3) + out]
 
@@ -996,8 +1003,33 @@ def tall_flush(cvt, dt):
     s0 = step_ds(dt, 0, zero_c=True, wait=w0)
     w1 = younger_than_dma_of(1, ctx + [s0])
     s1 = step_ds(dt, 1, wait=w1)
-    assert w0 <= 63 and w1 <= 63, (w0, w1)
-    return out + s0 + s1 + ["s_branch L_s2_%="]
+    # then one of the workgroup's zero chunks (%[vzero] lane s90, s90 <
+    # %[nzero]; else 32 dummy stores dropped by a zero-size descriptor, so
+    # the counts below hold either way): the empty rows' HBM writes overlap
+    # the k-loop instead of following it; steps 2 and 3 recounted too
+    z = ["s_cmp_lt_u32 s90, %[nzero]", "s_cselect_b32 s86, 0x7fffffff, 0",
+         "s_min_u32 s77, s90, 63", "s_add_u32 s90, s90, 1", "s_nop 3",
+         "v_readlane_b32 s76, %[vzero], s77",
+         "s_and_b32 s77, s76, 0xffff",
+         "s_mul_i32 s84, s77, %[crow]", "s_mul_hi_u32 s85, s77, %[crow]",
+         "s_add_u32 s84, s84, %[cdlo]", "s_addc_u32 s85, s85, %[cdhi]",
+         "s_lshr_b32 s77, s76, 16", "s_lshl_b32 s77, s77, 10",
+         "s_add_u32 s84, s84, s77", "s_addc_u32 s85, s85, 0",
+         "s_mov_b32 s87, 0x00020000", "s_mov_b32 s78, 0"]
+    z += [f"v_mov_b32 v{96 + j}, 0" for j in range(4)]
+    for _ in range(32):
+        z += ["buffer_store_dwordx4 v[96:99], %[vco], s[84:87], s78 offen nt",
+              "s_add_u32 s78, s78, %[c4]"]
+    w2 = younger_than_dma_of(2, ctx + [s0, s1 + z])
+    s2 = step_ds(dt, 2, wait=w2)
+    w3 = younger_than_dma_of(3, ctx + [s0, s1 + z, s2])
+    s3 = step_ds(dt, 3, wait=w3)
+    assert max(w0, w1, w2, w3) <= 63, (w0, w1, w2, w3)
+    tail = []
+    if stamps:
+        tail = ["s_memrealtime s[98:99]", "s_waitcnt lgkmcnt(0)",
+                "s_sub_u32 s98, s98, s96", "s_add_u32 s89, s89, s98"]
+    return out + s0 + s1 + z + s2 + s3 + tail + ["s_branch L_blkend_%="]
 
 
 KS_CHUNKS = (2, 4, 8)
@@ -1145,6 +1177,10 @@ def _build(dt, wave_epi, last_block, stamps):
     and %[r4] (a producer's publish start and end)."""
     cvt = f"v_cvt_pk_{dt}_f32"
     body = prologue()
+    if VARIANT["tp"]:  # zero chunks done in the loop
+        body.append("s_mov_b32 s90, 0")
+    if stamps and VARIANT["tp"]:
+        body += ["s_mov_b32 s88, 0", "s_mov_b32 s89, 0"]
     if stamps:
         body.append("s_memrealtime %[r0]")
     # the first block's step 0 is the zero-C copy below (L_first)
@@ -1163,6 +1199,8 @@ def _build(dt, wave_epi, last_block, stamps):
                          "s_cmp_eq_u32 s61, %[publast]", "s_cbranch_scc1 L_publ_%="]
             body.append("L_s3_%=:")
         body += step(dt, H)
+    if VARIANT["tp"]:
+        body.append("L_blkend_%=:")
     body.append("s_sub_u32 s61, s61, 1")
     if VARIANT["tp"]:  # the block just done ends its tile: store the tile
         body += ["s_sub_u32 s74, %[ntot], s61", "s_sub_u32 s74, s74, 1", "s_nop 3",
@@ -1257,7 +1295,7 @@ def _build(dt, wave_epi, last_block, stamps):
     body += epilogue_body(cvt, "collect", wave_epi)
     body.append("s_branch L_done_%=")
     if VARIANT["tp"]:
-        body += tall_flush(cvt, dt)
+        body += tall_flush(cvt, dt, stamps)
     if VARIANT["ks"]:
         body += ksplit()
         for S in KS_CHUNKS:
@@ -1270,6 +1308,8 @@ def _build(dt, wave_epi, last_block, stamps):
     if VARIANT["bar2"] or VARIANT["il"]:
         body.append("L_end_%=:")
     body.append("L_fin_%=:")
+    if stamps and VARIANT["tp"]:
+        body.append("s_mov_b64 %[r3], s[88:89]")
     if stamps:
         body += ["s_memrealtime %[r2]", "s_waitcnt lgkmcnt(0)"]
     return body
@@ -1362,7 +1402,7 @@ def render():
             lines += ['  ""', ""]
     clob = ([f'"a{i}"' for i in range(256)] + [f'"v{i}"' for i in range(96, 256)]
             + [f'"s{i}"' for i in range(40, 48)] + [f'"s{i}"' for i in range(56, 80)]
-            + [f'"s{i}"' for i in range(84, 88)] + [f'"s{i}"' for i in range(96, 100)]
+            + [f'"s{i}"' for i in range(84, 91)] + [f'"s{i}"' for i in range(96, 100)]
             + ['"scc"', '"vcc"', '"memory"'])
     lines.append("#define DSD4W_CLOBBERS " + ", ".join(clob))
     return "\n".join(lines) + "\n"
