@@ -91,6 +91,7 @@ enum KnobId {
   kKnobSddKsplitMinK,
   kKnobSddOrder,
   kKnobTall4w,
+  kKnobTallFlushW,
   kNumKnobs
 };
 int Knob(KnobId k);

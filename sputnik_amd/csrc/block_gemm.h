@@ -208,6 +208,9 @@ struct GemmParams {
   // Grouped SDD on the 4-wave kernel, every row the same group count:
   // 0 group-major order, 1 blocks of 8 rows x 4 groups (dsd4w.hip).
   int sdd_order;
+  // Tall DSD pipeline (dsd4w.hip kEpi 7): weight of a tile's store in
+  // quarter blocks (the cost-balanced cut of the block sequence).
+  int tall_flush_w;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

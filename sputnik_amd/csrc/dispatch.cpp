@@ -115,6 +115,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
     {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
     {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
+    {"tall_flush_w", "SPUTNIK_AMD_TALL_FLUSH_W", 4, 0, 64},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1036,8 +1037,11 @@ static bool UseTallPipe(const GemmParams &p, long long blocks, long long row_max
   if (cus <= 0) return false;
   // blocks per workgroup: a weighted share (a tile weighs its blocks + 1:
   // blocks + non-empty rows per panel) plus the tile the cut runs into
+  // (weight w quarter blocks per tile: blocks + w / 4 x non-empty rows)
+  const long long fw = Knob(kKnobTallFlushW);
   const long long per =
-      ((blocks + std::min<long long>(blocks, p.num_rows)) * (p.j_limit / 512) + cus - 1) / cus;
+      ((4 * blocks + fw * std::min<long long>(blocks, p.num_rows)) * (p.j_limit / 512) +
+       4LL * cus - 1) / (4LL * cus);
   // (the empty rows' zero chunks: an equal share of at most panels x rows)
   const long long zero_per = ((long long)(p.j_limit / 512) * p.num_rows + cus - 1) / cus;
   return per + row_max <= 128 && zero_per <= 64 && blocks < (1LL << 24) &&
@@ -1065,6 +1069,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     GemmParams q = p0;
     q.persistent = 0;
     q.num_jtiles = q.j_limit / 512;
+    q.tall_flush_w = Knob(kKnobTallFlushW);
     int dev = 0;
     q.num_tiles = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
     return LaunchDsd4w(dtype, q, 7, false, stream, false, false);
