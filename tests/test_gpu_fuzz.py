@@ -396,3 +396,63 @@ def test_fuzz_sdd(kind, R, NB, K, trans):
         ref = O.gemm(np.ascontiguousarray(av[r * B:(r + 1) * B]), False,
                      np.ascontiguousarray(bv[:, c * B:(c + 1) * B]), False)
         H.assert_close(got[e], ref, dtype, f"sdd {trans} {kind} block {e}")
+
+
+# -------------------------------------------------------------- tall DSD --
+
+TALL_CASES = [
+    # kind, R (block-rows, > 256: tall), KB, N, unaligned
+    ("skewed", 320, 16, 2048, False),
+    ("last0", 300, 8, 1024, True),
+    ("odd_last1", 280, 32, 512, False),
+]
+
+
+@pytest.mark.parametrize("kind,R,KB,N,unaligned", TALL_CASES)
+def test_fuzz_dsd_tall_pipe(kind, R, KB, N, unaligned):
+    """Tall DSD NN on the 4-wave pipeline (plan 4, dsd4w.hip kEpi 7) against
+    the 8-wave tall tile (knob tall4w = 0) and the oracle: random values,
+    skewed / empty / 1-block rows, an index list off 16-byte alignment.
+    The two kernels sum each 128 x 128 block's k-blocks in the same order
+    (CSR order, 32-deep MFMA steps), so they agree bit for bit."""
+    seed = _seed("tall", kind, R, KB, N, unaligned)
+    rng = np.random.default_rng(seed)
+    M, K = R * B, KB * B
+    off, idx = row_topology(kind, R, KB, rng)
+    nb = int(off[-1])
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    a = rnd(nb * B * B, g, torch.float16)
+    b = rnd(K * N, g, torch.float16)
+    A = sp.BlockMatrix(M, K, B, nb * B * B, a,
+                       torch.from_numpy(off.astype(np.int32)).cuda(),
+                       dev_index(idx, unaligned))
+    Bm = sp.Matrix(K, N, b)
+
+    def go(tall4w):
+        prev = sp.tuning("tall4w", tall4w)
+        try:
+            c = torch.full((M, N), float("nan"), dtype=torch.float16, device="cuda")
+            plan = sp.dsd_plan(A, False, Bm, False, sp.Matrix(M, N, c))
+            sp.Matmul(A, False, Bm, False, sp.Matrix(M, N, c))
+            torch.cuda.synchronize()
+            return c, plan
+        finally:
+            sp.tuning("tall4w", prev)
+    got, plan = go(1)
+    ref8, plan8 = go(0)
+    assert plan == 4 and plan8 == 2, (plan, plan8)
+    assert not torch.isnan(got.float()).any()
+    assert torch.equal(got, ref8), float((got.float() - ref8.float()).abs().max())
+    av = a.float().cpu().numpy()[: max(nb, 1) * B * B].reshape(-1, B, B)[:nb]
+    bv = b.float().cpu().numpy().reshape(K, N)
+    counts = np.diff(off)
+    rows = sorted(set([0, R - 1, int(np.argmax(counts))] +
+                      [int(x) for x in rng.choice(R, 5, replace=False)]))
+    for r in rows:
+        o0, o1 = off[r], off[r + 1]
+        a_row = mu.to_dense(128, K, np.array([0, o1 - o0], np.int32), idx[o0:o1], av[o0:o1])
+        ref = O.gemm(a_row, False, bv, False, threads=H.oracle_threads())
+        H.assert_close(got[r * B:(r + 1) * B].float().cpu().numpy(), ref, "f16",
+                       f"tall {kind} row-block {r}")
+
