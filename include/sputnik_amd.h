@@ -214,8 +214,9 @@ int sputnik_select_dsd_kernel(int four_wave);
  * (0), "sdd4w_max_ld" (16384), "pair_fault" (0), "sdd_ksplit" (8: most
  * K-split chunks, 1 off), "sdd_ksplit_min_k" (6144), "sdd_order" (1),
  * "tall4w" (1: the tall DSD NN pipeline), "tall_flush_w" (4: a tile
- * store's weight in quarter blocks for the pipeline's work split). get
- * returns the value,
+ * store's weight in quarter blocks for the pipeline's work split),
+ * "tall_odd_share" (120: an odd XCD's workgroup share in percent of an even
+ * one's). get returns the value,
  * set the previous value; both return INT_MIN for an unknown name, set also
  * for a value out of the knob's range (nothing changes then). */
 int sputnik_tuning_get(const char *name);

@@ -1,0 +1,60 @@
+"""Same-process A/B of one tuning knob on one bench workload problem:
+python scripts/exp_knob_ab.py KNOB v1,v2,... [--workload panel|dsd] [--density D]
+Interleaved rounds, median per value (us)."""
+import argparse
+import json
+import os
+import sys
+import types
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import sputnik_amd as sp  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("knob")
+    ap.add_argument("values")
+    ap.add_argument("--workload", default="panel")
+    ap.add_argument("--density", type=float, default=0.5)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=30)
+    a = ap.parse_args()
+    vals = [int(v) for v in a.values.split(",")]
+    dev = torch.device("cuda", 0)
+    args = types.SimpleNamespace(seed=0, k=4096, n=4096, m=4096, dtype="f16")
+    if a.workload == "panel":
+        prob = bench.dsd_panel(args, 1, 0, dev, 0.02, m_total=131072)
+    else:
+        prob = bench.dsd_panel(args, 1, 0, dev, a.density, m_total=4096)
+    res = {v: [] for v in vals}
+    prev = sp.tuning(a.knob)
+    try:
+        for _ in range(a.rounds):
+            for v in vals:
+                sp.tuning(a.knob, v)
+                fn = prob.launcher()
+                for _ in range(5):
+                    fn()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(a.iters):
+                    fn()
+                e.record()
+                torch.cuda.synchronize()
+                res[v].append(s.elapsed_time(e) * 1e3 / a.iters)
+    finally:
+        sp.tuning(a.knob, prev)
+    out = {"knob": a.knob, "workload": a.workload,
+           "us_median": {v: round(sorted(x)[len(x) // 2], 2) for v, x in res.items()},
+           "us_min": {v: round(min(x), 2) for v, x in res.items()}}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

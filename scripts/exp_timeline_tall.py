@@ -44,6 +44,23 @@ def main():
            "after_flush_2steps_sum": stats(us(t[has, 9] >> 32)),
            "zero_fill": stats(us(t[:, 15] - np.where(t[:, 4] > 0, t[:, 4], t[:, 0]))),
            "end": stats(us(t[:, 15] - e0))}
+    # per XCD (workgroup b runs on XCD b % 8 under round-robin dispatch):
+    # k-loop time per block and end; and the slowest workgroups' shapes
+    bid = np.nonzero(buf.view(-1, 16).cpu().numpy()[:, 0] > 0)[0]
+    xcd = bid % 8
+    comp = us(t[:, 4] - t[:, 2])
+    out["by_xcd"] = {int(x): {"compute_p50": round(float(np.median(comp[xcd == x])), 1),
+                              "compute_max": round(float(comp[xcd == x].max()), 1),
+                              "blocks_sum": int(t[xcd == x, 5].sum()),
+                              "tiles_sum": int(t[xcd == x, 14].sum())}
+                     for x in range(8)}
+    order = np.argsort(-comp)[:10]
+    out["slowest"] = [[round(float(comp[i]), 1), int(t[i, 5]), int(t[i, 14]), int(xcd[i]),
+                       int(bid[i])] for i in order]
+    out["fastest"] = [[round(float(comp[i]), 1), int(t[i, 5]), int(t[i, 14]), int(xcd[i]),
+                       int(bid[i])] for i in np.argsort(comp)[:6]]
+    c = np.corrcoef(comp, t[:, 14])[0, 1] if len(t) > 2 else 0.0
+    out["corr_compute_tiles"] = round(float(c), 3)
     print(json.dumps(out), flush=True)
 
 

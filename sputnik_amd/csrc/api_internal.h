@@ -92,6 +92,7 @@ enum KnobId {
   kKnobSddOrder,
   kKnobTall4w,
   kKnobTallFlushW,
+  kKnobTallOddShare,
   kNumKnobs
 };
 int Knob(KnobId k);

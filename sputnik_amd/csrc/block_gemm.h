@@ -211,6 +211,7 @@ struct GemmParams {
   // Tall DSD pipeline (dsd4w.hip kEpi 7): weight of a tile's store in
   // quarter blocks (the cost-balanced cut of the block sequence).
   int tall_flush_w;
+  int tall_odd_share;  // ... and an odd XCD's workgroup share, percent of an even one's
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

@@ -116,6 +116,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
     {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
     {"tall_flush_w", "SPUTNIK_AMD_TALL_FLUSH_W", 4, 0, 64},
+    {"tall_odd_share", "SPUTNIK_AMD_TALL_ODD_SHARE", 120, 50, 200},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1042,9 +1043,14 @@ static bool UseTallPipe(const GemmParams &p, long long blocks, long long row_max
   const long long per =
       ((4 * blocks + fw * std::min<long long>(blocks, p.num_rows)) * (p.j_limit / 512) +
        4LL * cus - 1) / (4LL * cus);
-  // (the empty rows' zero chunks: an equal share of at most panels x rows)
-  const long long zero_per = ((long long)(p.j_limit / 512) * p.num_rows + cus - 1) / cus;
-  return per + row_max <= 128 && zero_per <= 64 && blocks < (1LL << 24) &&
+  // (the empty rows' zero chunks: a share of at most panels x rows; the
+  // odd-XCD share scales both by up to 2 max(odd, 100) / (100 + odd))
+  const long long odd = Knob(kKnobTallOddShare), big = std::max<long long>(odd, 100);
+  const long long zero_per =
+      ((long long)(p.j_limit / 512) * p.num_rows * 2 * big + cus * (100 + odd) - 1) /
+      (cus * (100 + odd));
+  const long long per_x = (per * 2 * big + (100 + odd) - 1) / (100 + odd) + 1;
+  return per_x + row_max <= 128 && zero_per <= 63 && blocks < (1LL << 24) &&
          p.j_limit / 512 < 256;
 }
 
@@ -1070,6 +1076,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     q.persistent = 0;
     q.num_jtiles = q.j_limit / 512;
     q.tall_flush_w = Knob(kKnobTallFlushW);
+    q.tall_odd_share = Knob(kKnobTallOddShare);
     int dev = 0;
     q.num_tiles = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
     return LaunchDsd4w(dtype, q, 7, false, stream, false, false);
