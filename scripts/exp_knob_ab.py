@@ -29,6 +29,15 @@ def main():
     args = types.SimpleNamespace(seed=0, k=4096, n=4096, m=4096, dtype="f16")
     if a.workload == "panel":
         prob = bench.dsd_panel(args, 1, 0, dev, 0.02, m_total=131072)
+    elif a.workload in ("dds", "pair"):  # config 3's DDS (g . C) or the whole pair
+        pp = bench.PairProblem(4096, a.density, "f16", 7, dev)
+        if a.workload == "pair":
+            prob = pp
+        else:
+            cg = sp.Matrix(4096, 4096, pp.g)
+            co = sp.Matrix(4096, 4096, pp.out)
+            prob = types.SimpleNamespace(
+                launcher=lambda: (lambda: sp.MatmulEx(cg, False, pp.C, False, co)))
     else:
         prob = bench.dsd_panel(args, 1, 0, dev, a.density, m_total=4096)
     res = {v: [] for v in vals}

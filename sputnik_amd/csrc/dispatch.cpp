@@ -108,7 +108,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"grouped_min_per_cu", "SPUTNIK_AMD_GROUPED_MIN_PER_CU", 5, 0, 1 << 20},
     {"tall", "SPUTNIK_AMD_TALL", 1, 0, 2},
     {"tall_persistent", "SPUTNIK_AMD_TALL_PERSISTENT", 1, 0, 1},
-    {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 0, 0, 3},
+    {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 3, 0, 3},
     {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 16384, 0, 1 << 30},
     {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
     {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
@@ -1114,7 +1114,9 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   if (Dsd4wEnabled() &&
       Dds4wApplies(p, Dsd4wForced() ? (1LL << 40) : b.nonzeros / (kBlock * kBlock),
                    tb, !ta, true, tall)) {
-    // (the two-panel pair placement: DSD-measured; DDS experiment knob)
+    // (the two-panel pair placement, heavy pairs on the odd XCDs: DDS NN
+    // A/B r05 dx, same process, mode 0 -> 3: 10% 24.49 -> 24.41, 20% 32.44
+    // -> 32.33, 30% 40.03 -> 38.69, 50% 56.75 -> 55.06, 90% 89.76 -> 87.64 us)
     if (p.pair_xcd2 != 0) p.pair_xcd2 = Knob(kKnobDdsXcd2);
     return LaunchDds4w(dtype, p, Dsd4wEpi(), tb && !ta, stream, ta && !tb, ta && tb);
   }
