@@ -38,6 +38,11 @@ def main():
             co = sp.Matrix(4096, 4096, pp.out)
             prob = types.SimpleNamespace(
                 launcher=lambda: (lambda: sp.MatmulEx(cg, False, pp.C, False, co)))
+    elif a.workload.startswith("op:"):  # op:OP:TRANS:DIM, e.g. op:sdd:NN:4096
+        _, op, tr, dim = a.workload.split(":")
+        oa = types.SimpleNamespace(k=int(dim), density=a.density, op=op, trans=tr,
+                                   seed=0, dtype="f16", api="ex")
+        prob = bench.OpProblem(oa, dev)
     else:
         prob = bench.dsd_panel(args, 1, 0, dev, a.density, m_total=4096)
     res = {v: [] for v in vals}
