@@ -155,7 +155,7 @@ const char *sputnik_version(void);
 const char *sputnik_build_hash(void);
 
 /* ---- Diagnostics (need a device) */
-/* SDD tile plan: 1 = grouped 128x512 tiles (>= 5 blocks per CU), 2 = the
+/* SDD tile plan: 1 = grouped 128x512 tiles (>= 4 blocks per CU), 2 = the
  * grouped tiles with each group's K split over 2-8 workgroups (SDD NN, few
  * groups: one workgroup per CU), 0 = one k-split 128x128 block per
  * workgroup, -1 = the problem is rejected. (Decides as a launch on the null
@@ -210,7 +210,7 @@ int sputnik_select_dsd_kernel(int four_wave);
 /* Tuning knobs, each initialised from its environment variable
  * SPUTNIK_AMD_<NAME> (upper case) or its default: "pairs" (1), "pair_xcd2"
  * (3), "split" (1), "split_min_bn" (128), "dsd4w" (1), "grouped_sdd" (1),
- * "grouped_min_per_cu" (5), "tall" (1), "tall_persistent" (1), "dds_xcd2"
+ * "grouped_min_per_cu" (4), "tall" (1), "tall_persistent" (1), "dds_xcd2"
  * (3), "sdd4w_max_ld" (16384), "pair_fault" (0), "sdd_ksplit" (8: most
  * K-split chunks, 1 off), "sdd_ksplit_min_k" (6144), "sdd_order" (1),
  * "tall4w" (1: the tall DSD NN pipeline), "tall_flush_w" (4: a tile

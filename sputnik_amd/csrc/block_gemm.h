@@ -1725,23 +1725,29 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         }
         int start = before + incl - local;
         const bool uniform = gmin == gmax;
+        // The grid is an upper bound on the groups: the first `total`
+        // workgroups take the groups, XCD-contiguous over `total` (not over
+        // the grid), so no XCD's share spills into a second round while the
+        // spare workgroups exit (dsd4w.hip, the same mapping).
+        const int gt = (SPUTNIK_EXP & 8) ? tile
+                       : (int)blockIdx.x < total ? xcd_tile(blockIdx.x, total) : total;
         if (!uniform) {
           for (int r = r0; r < r1; ++r) {
             const int g =
                 (p.c_offsets[r + 1] - p.c_offsets[r] + kGrp - 1) / kGrp;
-            if (tile >= start && tile < start + g) {
+            if (gt >= start && gt < start + g) {
               scratch[0] = r;
-              scratch[1] = tile - start;
+              scratch[1] = gt - start;
             }
             start += g;
           }
         }
         __syncthreads();
-        if (tile >= total) return;  // whole workgroup: no barrier pending
+        if (gt >= total) return;  // whole workgroup: no barrier pending
         int gi;
         if (uniform) {
-          srow = tile % R;
-          gi = tile / R;
+          srow = gt % R;
+          gi = gt / R;
         } else {
           srow = __builtin_amdgcn_readfirstlane(scratch[0]);
           gi = __builtin_amdgcn_readfirstlane(scratch[1]);

@@ -105,7 +105,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"split_min_bn", "SPUTNIK_AMD_SPLIT_MIN_BN", 128, 0, 1 << 20},
     {"dsd4w", "SPUTNIK_AMD_DSD4W", 1, 0, 7},
     {"grouped_sdd", "SPUTNIK_AMD_GROUPED_SDD", 1, 0, 1},
-    {"grouped_min_per_cu", "SPUTNIK_AMD_GROUPED_MIN_PER_CU", 5, 0, 1 << 20},
+    {"grouped_min_per_cu", "SPUTNIK_AMD_GROUPED_MIN_PER_CU", 4, 0, 1 << 20},
     {"tall", "SPUTNIK_AMD_TALL", 1, 0, 2},
     {"tall_persistent", "SPUTNIK_AMD_TALL_PERSISTENT", 1, 0, 1},
     {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 3, 0, 3},
@@ -113,7 +113,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
     {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
-    {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 1},
+    {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 4},
     {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
     {"tall_flush_w", "SPUTNIK_AMD_TALL_FLUSH_W", 4, 0, 64},
     {"tall_odd_share", "SPUTNIK_AMD_TALL_ODD_SHARE", 120, 50, 200},
@@ -846,12 +846,15 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
   if (hipGetDevice(&dev) != hipSuccess) return false;
   const int cus = DeviceCUs(dev);
   if (cus <= 0) return false;
-  // From 5 blocks per CU the grouped tile is faster (SDD 8192^2 x 8192,
-  // scripts/exp_grp.sh, r02: 4 per CU k-split 318 vs grouped 362 us; 5 per
-  // CU 399 vs 365; 6 per CU 491 vs 387; 8 per CU 652 vs 570).
-  // Knob "grouped_min_per_cu" (default 5) moves the switch (tuning only;
+  // From 4 blocks per CU the grouped tile is faster: the 4-wave grouped
+  // kernel with its groups mapped over the actual group count (r05 gm2,
+  // same process: SDD 4096^3 dense = 4 per CU, every transpose 100-103 us
+  // vs 158-164 us on the k-split tile; 2 per CU 77 vs 76, 3.2 per CU 286 vs
+  // 286: tie). r02's 8-wave grouped tile needed 5 per CU (scripts/
+  // exp_grp.sh: 4 per CU k-split 318 vs grouped 362 us, 5 per CU 399 vs 365).
+  // Knob "grouped_min_per_cu" (default 4) moves the switch (tuning only;
   // never below kGrp, so a grouped grid still fills every CU).
-  static_assert(5 >= kGrp, "a grouped grid fills every CU");
+  static_assert(4 >= kGrp, "a grouped grid fills every CU");
   const int min_per_cu = Knob(kKnobGroupedMinPerCu) < kGrp ? kGrp
                                                              : Knob(kKnobGroupedMinPerCu);
   if (blocks < min_per_cu * cus || p->num_rows > kMaxGroupRows)

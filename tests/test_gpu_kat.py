@@ -11,7 +11,7 @@ the same integer matrices (numpy on the host), converted exactly; the test
 is torch.equal on the whole output (value equality: +0 and -0 compare
 equal). The shapes reach every dispatch path: pair balancing (4096^2 with
 one tile per CU), tall operands, partial N/M/K tiles, the grouped SDD
-(>= 5 blocks per CU, checked with sputnik_sdd_plan), transposed metadata
+(>= 4 blocks per CU, checked with sputnik_sdd_plan), transposed metadata
 built by Matmul (device Transpose) and precomputed for MatmulEx.
 Reference test structure: sputnik/block/dsd/dsd_test.cu:68-194,
 sdd_test.cu:71-89 (same products, tolerance replaced by equality).
@@ -503,12 +503,12 @@ def test_sdd_plan_ksplit_default_gate():
 
 
 def test_sdd_plan_threshold():
-    """Just below 5 blocks per CU the k-split block tile is chosen, from 5
+    """Just below 4 blocks per CU the k-split block tile is chosen, from 4
     the grouped one (dispatch.cpp UseGroupedSdd)."""
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     rng = np.random.default_rng(1)
     side = 128 * 64
-    for nb, want in ((5 * cus - 1, 0), (5 * cus, 1)):
+    for nb, want in ((4 * cus - 1, 0), (4 * cus, 1)):
         A = IDense(side, 128, rng, "f16")
         Bd = IDense(128, side, rng, "f16")
         Cs = ISparse(side, side, None, rng, "f16", nb=nb)

@@ -387,7 +387,8 @@ def test_sdd_ragged_k(k):
 @pytest.mark.parametrize("k", [200, 1024])
 @pytest.mark.parametrize("dtype", ["f16", "bf16"])
 def test_sdd_grouped_tiles(k, dtype):
-    """Enough output blocks (5 x CUs + 37, dispatch.cpp UseGroupedSdd) for
+    """Enough output blocks (5 x CUs + 37 > the 4 x CUs of dispatch.cpp
+    UseGroupedSdd) for
     the grouped SDD tiles: up to 4 consecutive stored blocks of a block-row
     per workgroup, rows whose block counts are not multiples of 4, unordered
     columns, a K tail, all four transposes; every block against the oracle.
