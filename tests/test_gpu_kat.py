@@ -342,6 +342,25 @@ def test_kat_sdd_grouped(ta, tb, k):
     _equal(got, want, f"sdd grouped {ta}{tb} k={k}")
 
 
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("m,order", [(2048, 1), (1920, 1), (2048, 0)])
+def test_kat_sdd_grouped_pow2_stride(ta, tb, m, order):
+    """Grouped 4-wave SDD with 32-KiB rows (n = 16384, the power-of-two
+    stride the 8-wave kernel used to keep) over a random topology, in the
+    band order (sdd_order 1: bands of 8 rows group-index-major, 15 rows = a
+    partial last band) and row-major (0): every stored block written once."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    prev = sp.tuning("sdd_order")
+    sp.tuning("sdd_order", order)
+    try:
+        got, want, plan = kat_sdd(m, 256, 16384, None, ta, tb, "f16", nb=4 * cus + 37,
+                                  seed=m + order + 2 * ta + tb)
+    finally:
+        sp.tuning("sdd_order", prev)
+    assert plan == 1, "grouped SDD tiles not selected"
+    _equal(got, want, f"sdd pow2 {ta}{tb} m={m} order={order}")
+
+
 # (m, k, n, stored blocks, dtype): one CU's workgroup per chunk, S picked
 # in-kernel from the group count (dsd4w.hip kKs): 8 rows x 60 blocks with
 # K = 2048 -> S = 8 (2 k-blocks per chunk, many partial groups); 150 blocks,
