@@ -211,7 +211,7 @@ int sputnik_select_dsd_kernel(int four_wave);
  * SPUTNIK_AMD_<NAME> (upper case) or its default: "pairs" (1), "pair_xcd2"
  * (3), "split" (1), "split_min_bn" (128), "dsd4w" (1), "grouped_sdd" (1),
  * "grouped_min_per_cu" (4), "tall" (1), "tall_persistent" (1), "dds_xcd2"
- * (3), "sdd4w_max_ld" (2^30: off), "pair_fault" (0), "sdd_ksplit" (8: most
+ * (3), "sdd4w_max_ld" (16384), "pair_fault" (0), "sdd_ksplit" (8: most
  * K-split chunks, 1 off), "sdd_ksplit_min_k" (6144), "sdd_order" (1),
  * "tall4w" (1: the tall DSD NN pipeline), "tall_flush_w" (4: a tile
  * store's weight in quarter blocks for the pipeline's work split),

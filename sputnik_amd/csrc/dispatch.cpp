@@ -109,7 +109,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"tall", "SPUTNIK_AMD_TALL", 1, 0, 2},
     {"tall_persistent", "SPUTNIK_AMD_TALL_PERSISTENT", 1, 0, 1},
     {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 3, 0, 3},
-    {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 1 << 30, 0, 1 << 30},
+    {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 16384, 0, 1 << 30},
     {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
     {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
@@ -1138,7 +1138,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   const bool grouped = UseGroupedSdd(&p, c, tb);
   if (!grouped && PrepareSddKsplit(&p, c, ta, tb, stream))
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
-  if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb)) {
+  if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb, c.nonzeros / (kBlock * kBlock))) {
     p.sdd_order = Knob(kKnobSddOrder);
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
   }

@@ -55,7 +55,7 @@ hipError_t LaunchDds4w(int dtype, const GemmParams &p, int epi, bool nt,
 // Grouped SDD NN / NT / TT (dispatch.cpp UseGroupedSdd: up to 4 stored
 // blocks of a block-row per workgroup, grid = the group count's upper
 // bound), K a multiple of 128: dsd4w.hip kSdd / kNt / kTt.
-bool Sdd4wApplies(const GemmParams &p, bool grouped, bool ta, bool tb);
+bool Sdd4wApplies(const GemmParams &p, bool grouped, bool ta, bool tb, long long blocks = -1);
 hipError_t LaunchSdd4w(int dtype, const GemmParams &p, bool ta, bool tb, int epi,
                        hipStream_t stream);
 
