@@ -102,6 +102,10 @@ def parse():
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="HBM traffic per launch measured by rocprofv3 --pmc "
                          "(scripts/pmc.sh), keyed by shape and build hash")
+    ap.add_argument("--pmc-workloads",
+                    default=os.path.join(ROOT, "profiles", "pmc_workloads.json"),
+                    help="per-kernel PMC of the sdd_dds / moe / panel workloads "
+                         "(scripts/pmc_workload.sh), keyed by workload and build hash")
     return ap.parse_args()
 
 
@@ -175,6 +179,33 @@ def pmc_traffic(path, key, build_hash):
     return entry.get("hbm_bytes_per_launch"), "rocprofv3 --pmc, same build"
 
 
+def pmc_workload_traffic(path, workload, build_hash):
+    """L2<->fabric bytes of one step of a non-headline workload: the sum over
+    the library's kernels of a step (dsd4w_kernel / block_gemm launches; the
+    metadata kernels run before the timed region) of their per-launch bytes
+    from scripts/pmc_workload.sh, only when measured on this exact build.
+    -> (bytes or None, per-kernel dict, note)."""
+    try:
+        with open(path) as f:
+            entry = json.load(f).get(workload)
+    except (OSError, ValueError):
+        return None, None, "no workload PMC summary"
+    if not entry:
+        return None, None, f"no workload PMC entry for {workload}"
+    if entry.get("build_hash") != build_hash:
+        return None, None, (f"PMC entry measured on build {entry.get('build_hash')}, "
+                            f"not {build_hash}")
+    per = {k: {"bytes": v.get("hbm_bytes_per_launch"), "us": v.get("profiled_kernel_us"),
+               "mfma_busy_frac": v.get("mfma_busy_frac"), "l2_hit": v.get("l2_hit")}
+           for k, v in entry.get("kernels", {}).items()
+           if ("dsd4w_kernel" in k or "block_gemm" in k) and
+           v.get("hbm_bytes_per_launch") is not None}
+    if not per:
+        return None, None, "no library kernel in the workload PMC entry"
+    return (sum(v["bytes"] for v in per.values()), per,
+            "rocprofv3 --pmc (scripts/pmc_workload.sh), same build, summed over the step's kernels")
+
+
 PEAK_CLOCK_GHZ = 2.4  # MI355X peak engine clock (the 2.5 PF dense fp16 figure)
 
 
@@ -206,6 +237,31 @@ def pmc_clock(path, key, build_hash, achieved_tflops, peak_tflops):
 def _values(n, td, gen, device):
     import torch
     return (torch.rand(n, generator=gen, device=device) * 2 - 1).to(td)
+
+
+_SDD_KERNELS = {
+    0: "block_gemm_kernel (SDD, 8-wave k-split 128x128 block tile)",
+    1: "block_gemm_kernel (SDD, 8-wave grouped 128x512 tiles)",
+    2: "dsd4w_kernel (SDD NN, 4-wave grouped tiles, K split over workgroups)",
+    3: "dsd4w_kernel (SDD, 4-wave grouped 128x512 tiles)",
+}
+_DSD_KERNELS = {
+    0: "block_gemm_kernel ({op}, 8-wave 128x512 tile)",
+    1: "dsd4w_kernel ({op}, 4 waves of 128x128)",
+    2: "block_gemm_kernel ({op}, tall 128x256 x2 per CU)",
+    3: "block_gemm_kernel ({op}, split mode)",
+    4: "dsd4w_kernel ({op}, tall pipeline, persistent)",
+}
+
+
+def sdd_kernel_name(sp, a, ta, b, tb, c):
+    """The SDD kernel the dispatcher picks (sputnik_sdd_kernel)."""
+    return _SDD_KERNELS.get(sp.sdd_kernel(a, ta, b, tb, c), "rejected")
+
+
+def dsd_kernel_name(sp, op, plan):
+    """The DSD / DDS kernel of a dsd_plan / dds_plan code."""
+    return _DSD_KERNELS.get(plan, "rejected").format(op=op)
 
 
 def _td(dtype):
@@ -508,8 +564,12 @@ class PairProblem:
         self.anchor_shape = (dim, dim, int(round(dim * density)))
         self.bytes = 2 * (nz * 2 + 2 * dim * dim * 2) + nb * 8
         self.dtype_code = 0 if dtype == "f16" else 1
-        self.kernel = ("block_gemm_kernel (SDD, k-split 128x128 tile) + "
-                       "dsd4w_kernel (DDS NN, 4 waves)")
+        # (what the dispatcher actually picks: sputnik_sdd_kernel /
+        # sputnik_dds_plan)
+        X, W, G = (sp.Matrix(dim, dim, t) for t in (self.x, self.w, self.g))
+        self.kernel = (sdd_kernel_name(sp, X, False, W, False, self.C) + " + " +
+                       dsd_kernel_name(sp, "DDS NN", sp.dds_plan(
+                           G, False, self.C, False, sp.Matrix(dim, dim, self.out))))
         self.desc = (f"SDD(x,w)->C then DDS(g,C) block=128 M=K=N={dim} "
                      f"density={density} {dtype} (MatmulEx metadata)")
 
@@ -567,6 +627,10 @@ class MoeProblem:
                       2 * d_model * cols * 2)
         self.dtype_code = 0 if dtype == "f16" else 1
         self.dtype_name = dtype
+        X, W1 = sp.Matrix(tokens, d_model, self.x), sp.Matrix(d_model, cols, self.w1)
+        W2, Y = sp.Matrix(cols, d_model, self.w2), sp.Matrix(tokens, d_model, self.y)
+        self.kernel = (sdd_kernel_name(sp, X, False, W1, False, self.H) + " + " +
+                       dsd_kernel_name(sp, "DSD NN", sp.dsd_plan(self.H, False, W2, False, Y)))
         self.desc = (f"MoE {experts} experts tokens={tokens} d_model={d_model} "
                      f"d_ff={d_ff} {dtype}: SDD(x,w1)->h + DSD(h,w2)")
 
@@ -633,11 +697,15 @@ class OpProblem:
                      f"density={dens} {args.dtype} "
                      f"({'MatmulEx' if args.api == 'ex' else 'Matmul'}"
                      f"{', device Transpose in every step' if meta_t and args.api == 'matmul' else ''})")
-        # (dispatch.cpp picks: the 4-wave dsd4w_kernel for every DSD / DDS
-        # transpose on one-tile-per-CU or split launches and the grouped
-        # SDD, block_gemm_kernel otherwise)
-        self.kernel = (f"{op.upper()} {args.trans} {args.dtype}: dsd4w_kernel where it "
-                       f"applies, else block_gemm_kernel")
+        # (what the dispatcher picks for this problem)
+        X, O_ = sp.Matrix(d, d, self.x), sp.Matrix(d, d, self.out)
+        tr = f"{op.upper()} {args.trans}"
+        if op == "dsd":
+            self.kernel = dsd_kernel_name(sp, tr, sp.dsd_plan(self.S, ta, X, tb, O_))
+        elif op == "dds":
+            self.kernel = dsd_kernel_name(sp, tr, sp.dds_plan(X, ta, self.S, tb, O_))
+        else:
+            self.kernel = sdd_kernel_name(sp, X, ta, sp.Matrix(d, d, self.y), tb, self.S)
 
     def launcher(self):
         import torch
@@ -780,8 +848,16 @@ def run_other(args, world, rank, device, build):
         value, unit, hib = per * 1e3, "us", False
     else:
         value, unit, hib = flops_all / (per * 1e-3) / 1e12, "TFLOP/s", True
+        traffic, per_kernel, note = (None, None, "not measured for this workload")
+        if args.workload in ("sdd_dds", "moe", "panel") and world == 1:
+            traffic, per_kernel, note = pmc_workload_traffic(
+                args.pmc_workloads, args.workload, build.get("hash"))
         extra["roofline"] = roofline(prob.flops, prob.bytes, per * 1e-3,
-                                     getattr(prob, "kernel", "block_gemm_kernel"))
+                                     getattr(prob, "kernel", "block_gemm_kernel"),
+                                     traffic)
+        extra["roofline"]["traffic_source"] = note
+        if per_kernel:
+            extra["roofline"]["traffic_kernels"] = per_kernel
         shape = getattr(prob, "anchor_shape", None)
         if rank == 0 and shape is not None:
             anchor = dense_anchor(*shape, getattr(prob, "dtype_name", args.dtype),

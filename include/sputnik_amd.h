@@ -163,6 +163,18 @@ const char *sputnik_build_hash(void);
 int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_block_matrix_t *c);
+/* The SDD kernel behind that plan: 0 = the 8-wave k-split block tile,
+ * 1 = grouped tiles on the 8-wave kernel, 2 = the 4-wave K-split, 3 =
+ * grouped tiles on the 4-wave kernel, -1 = rejected. */
+int sputnik_sdd_kernel(const sputnik_matrix_t *a, int transpose_a,
+                       const sputnik_matrix_t *b, int transpose_b,
+                       const sputnik_block_matrix_t *c);
+/* DDS kernel plan of a problem launched on `stream` (no launch, nothing
+ * allocated): 0 = the 8-wave 128x512 tile, 1 = the 4-wave kernel, 2 = the
+ * tall configuration, 3 = split mode (8-wave), -1 = rejected. */
+int sputnik_dds_plan(const sputnik_matrix_t *a, int transpose_a,
+                     const sputnik_block_matrix_t *b, int transpose_b,
+                     const sputnik_matrix_t *c, hipStream_t stream);
 /* DSD kernel plan of a problem launched on `stream` (no launch; makes the
  * launch's workspace decisions): 0 = the 8-wave 128x512 tile, 1 = the
  * 4-wave hand-scheduled kernel, 2 = the tall configuration, 3 = split mode,
@@ -211,12 +223,15 @@ int sputnik_select_dsd_kernel(int four_wave);
  * SPUTNIK_AMD_<NAME> (upper case) or its default: "pairs" (1), "pair_xcd2"
  * (3), "split" (1), "split_min_bn" (128), "dsd4w" (1), "grouped_sdd" (1),
  * "grouped_min_per_cu" (4), "tall" (1), "tall_persistent" (1), "dds_xcd2"
- * (3), "sdd4w_max_ld" (16384), "pair_fault" (0), "sdd_ksplit" (8: most
- * K-split chunks, 1 off), "sdd_ksplit_min_k" (6144), "sdd_order" (1),
+ * (3), "sdd4w_max_ld" (16384), "pair_fault" (0), "sdd_ksplit" (1: off;
+ * 2-8 the most K-split chunks -- its chunks wait on each other, so only
+ * where the launch has the device to itself),
+ * "sdd_ksplit_min_k" (6144), "sdd_order" (1),
  * "tall4w" (1: the tall DSD NN pipeline), "tall_flush_w" (4: a tile
  * store's weight in quarter blocks for the pipeline's work split),
  * "tall_odd_share" (120: an odd XCD's workgroup share in percent of an even
- * one's). get returns the value,
+ * one's). An environment value that does not parse or is out of range
+ * means the default. get returns the value,
  * set the previous value; both return INT_MIN for an unknown name, set also
  * for a value out of the knob's range (nothing changes then). */
 int sputnik_tuning_get(const char *name);

@@ -49,6 +49,9 @@ if [ "$PMC" != "-" ]; then
   fatal $rc && exit $rc
   bash scripts/pmc_workload.sh $TAG panel "--workload panel"; rc=$?
   fatal $rc && exit $rc
+  bash scripts/pmc_workload.sh $TAG moe "--workload moe"; rc=$?
+  fatal $rc && exit $rc
+  python3 scripts/pmc_merge_workloads.py $OUT $OUT/pmc_workloads.json
 fi
 if [ "$AB" != "-" ]; then
   bash scripts/exp_run.sh $TAG "$AB"; rc=$?

@@ -120,6 +120,8 @@ _SIGNATURES = {
     "sputnik_tuning_get": [ctypes.c_char_p],
     "sputnik_tuning_set": [ctypes.c_char_p, ctypes.c_int],
     "sputnik_dsd_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P],
+    "sputnik_sdd_kernel": [_P, ctypes.c_int, _P, ctypes.c_int, _P],
+    "sputnik_dds_plan": [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P],
 }
 _RESTYPES = {
     "sputnik_abi_block_matrix_size": ctypes.c_size_t,
@@ -364,6 +366,28 @@ def sdd_plan(a, transpose_a, b, transpose_b, c) -> int:
                                       ctypes.byref(cc)))
 
 
+def sdd_kernel(a, transpose_a, b, transpose_b, c) -> int:
+    """The kernel behind sdd_plan's tile plan: 0 8-wave k-split block tile,
+    1 8-wave grouped, 2 4-wave K-split, 3 4-wave grouped, -1 rejected
+    (sputnik_sdd_kernel)."""
+    ca, cb, cc = a._c(), b._c(), c._c()
+    return int(lib().sputnik_sdd_kernel(ctypes.byref(ca), int(bool(transpose_a)),
+                                        ctypes.byref(cb), int(bool(transpose_b)),
+                                        ctypes.byref(cc)))
+
+
+def dds_plan(a, transpose_a, b, transpose_b, c, stream=None) -> int:
+    """Kernel a DDS launch on `stream` would use: 0 8-wave tile, 1 4-wave
+    kernel, 2 tall, 3 split (8-wave), -1 rejected (sputnik_dds_plan)."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream().cuda_stream
+    ca, cb, cc = a._c(), b._c(), c._c()
+    return int(lib().sputnik_dds_plan(ctypes.byref(ca), int(bool(transpose_a)),
+                                      ctypes.byref(cb), int(bool(transpose_b)),
+                                      ctypes.byref(cc), ctypes.c_void_p(stream)))
+
+
 def pair_errors() -> int:
     """Pair hand-offs since the last call whose consumer timed out (its
     output tile is NaN; sputnik_pair_errors() in include/sputnik_amd.h)."""
@@ -475,7 +499,8 @@ from .gather import (allgather_concat, gather_block_runs,  # noqa: E402
 __all__ = [
     "AllocateBitmaskBuffers", "AllocateRowIndicesBuffer",
     "AllocateTransposeBuffers", "AsInt", "Bitmask", "FreeBitmaskBuffers",
-    "build_hash", "capture_workspaces", "pair_errors", "sdd_plan",
+    "build_hash", "capture_workspaces", "pair_errors", "sdd_plan", "sdd_kernel",
+    "dds_plan",
     "select_dsd_kernel", "dsd_plan", "tuning",
     "BlockMatrix", "BlockSize", "ExpertTopology", "FreeRowIndicesBuffer",
     "MaskToBcsr",

@@ -52,6 +52,13 @@ bool CanImplement(int op, const void *a, bool ta, const void *b, bool tb,
 // k-split 128x128 block per workgroup, -1 = rejected. Reads the CU count of
 // the current device (no launch).
 int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c);
+// SDD kernel (dispatch.cpp SddKernel): 0 8-wave k-split tile, 1 8-wave
+// grouped, 2 4-wave K-split, 3 4-wave grouped, -1 rejected.
+int SddKernel(const void *a, bool ta, const void *b, bool tb, const void *c);
+// DDS kernel plan (dispatch.cpp DdsPlan): 0 8-wave tile, 1 4-wave kernel,
+// 2 tall, 3 split (8-wave), -1 rejected.
+int DdsPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
+            hipStream_t stream);
 // DSD kernel plan (dispatch.cpp DsdPlan): 0 8-wave tile, 1 4-wave kernel,
 // 2 tall, 3 split mode, 4 tall pipeline, -1 rejected.
 int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,

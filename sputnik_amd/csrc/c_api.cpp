@@ -263,6 +263,26 @@ int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                               &cc);
 }
 
+int sputnik_sdd_kernel(const sputnik_matrix_t *a, int transpose_a,
+                       const sputnik_matrix_t *b, int transpose_b,
+                       const sputnik_block_matrix_t *c) {
+  if (!a || !b || !c) return -1;
+  const Matrix ca = ToCpp(a), cb = ToCpp(b);
+  const BlockMatrix cc = ToCpp(c);
+  return sputnik_amd::SddKernel(&ca, transpose_a != 0, &cb, transpose_b != 0,
+                                &cc);
+}
+
+int sputnik_dds_plan(const sputnik_matrix_t *a, int transpose_a,
+                     const sputnik_block_matrix_t *b, int transpose_b,
+                     const sputnik_matrix_t *c, hipStream_t stream) {
+  if (!a || !b || !c) return -1;
+  const Matrix ca = ToCpp(a), cc = ToCpp(c);
+  const BlockMatrix cb = ToCpp(b);
+  return sputnik_amd::DdsPlan(&ca, transpose_a != 0, &cb, transpose_b != 0, &cc,
+                              stream);
+}
+
 int sputnik_dsd_plan(const sputnik_block_matrix_t *a, int transpose_a,
                      const sputnik_matrix_t *b, int transpose_b,
                      const sputnik_matrix_t *c, hipStream_t stream) {

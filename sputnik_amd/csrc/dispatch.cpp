@@ -111,7 +111,9 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"dds_xcd2", "SPUTNIK_AMD_DDS_XCD2", 3, 0, 3},
     {"sdd4w_max_ld", "SPUTNIK_AMD_SDD4W_MAX_LD", 16384, 0, 1 << 30},
     {"pair_fault", "SPUTNIK_AMD_PAIR_FAULT", 0, 0, 1},
-    {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 8, 1, 8},
+    // (off by default: every chunk of a K-split group waits for all of its
+    // peers, so it needs the whole grid resident at once -- PrepareSddKsplit)
+    {"sdd_ksplit", "SPUTNIK_AMD_SDD_KSPLIT", 1, 1, 8},
     {"sdd_ksplit_min_k", "SPUTNIK_AMD_SDD_KSPLIT_MIN_K", 6144, 512, 1 << 30},
     {"sdd_order", "SPUTNIK_AMD_SDD_ORDER", 1, 0, 4},
     {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
@@ -126,8 +128,12 @@ static void InitKnobs() {
   std::call_once(g_knobs_once, [] {
     for (int i = 0; i < kNumKnobs; ++i) {
       const char *e = std::getenv(kKnobs[i].env);
-      int v = e != nullptr ? std::atoi(e) : kKnobs[i].def;
-      v = v < kKnobs[i].lo ? kKnobs[i].lo : v > kKnobs[i].hi ? kKnobs[i].hi : v;
+      // (an unset, unparsable or out-of-range value means the default)
+      char *end = nullptr;
+      const long v0 = e != nullptr && *e != 0 ? std::strtol(e, &end, 10) : 0;
+      const bool ok = e != nullptr && *e != 0 && end != nullptr && *end == 0 &&
+                      v0 >= kKnobs[i].lo && v0 <= kKnobs[i].hi;
+      const int v = ok ? (int)v0 : kKnobs[i].def;
       g_knobs[i].store(v, std::memory_order_relaxed);
     }
   });
@@ -285,9 +291,6 @@ static bool PairsEnabled() {
 // from 7% up, same-process A/B r01l).
 #ifndef SPUTNIK_PAIR_MIN_MEAN4
 #define SPUTNIK_PAIR_MIN_MEAN4 8  // 4 x mean blocks per row
-#endif
-#ifndef SPUTNIK_PAIR_XCD2_DEFAULT
-#define SPUTNIK_PAIR_XCD2_DEFAULT 3
 #endif
 // dry: decide only (DsdPlan): no workspace is allocated, re-tied or
 // advanced, and the pointers stay null.
@@ -876,7 +879,16 @@ bool UseGroupedSdd(GemmParams *p, const BlockMatrix &c, bool d_kc) {
 // actual group count), the partials reduced through the pair workspace.
 // Grid = one workgroup per CU, all resident at once (one 160-KiB-LDS
 // workgroup fits a CU): every chunk of a group is running while its peers
-// wait for it.
+// wait for it. That all-to-all wait is why it is OFF by default (knob
+// sdd_ksplit = 1): a launch that shares the device with another
+// kernel holding CUs for longer than the 0.2 s bounded wait (an RCCL kernel
+// on a side stream, a CU-masked stream) would leave chunks undispatched
+// while their peers time out, and the launch would return NaN tiles (counted
+// by sputnik_pair_errors()). Unlike the DSD pair hand-off -- a consumer waits
+// only on a producer dispatched before it -- no chunk order avoids this, and
+// a last-arriver reduction would serialize S - 1 partials on one CU (the
+// gain at K = 8192 was 5%). Opt in with sputnik_tuning_set("sdd_ksplit", 8)
+// when the launch has the device to itself.
 // dry: decide only (SddPlan), no workspace allocated, re-tied or advanced.
 static bool PrepareSddKsplit(GemmParams *p, const BlockMatrix &c, bool ta, bool tb,
                              hipStream_t stream, bool dry = false) {
@@ -1072,7 +1084,10 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   p.debug = g_debug;
   PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
   const GemmParams p0 = p;  // (before the tall configuration)
-  const bool tall = UseTall(&p, stream);
+  // decide without allocating first: the tall pipeline needs no persistent
+  // tile counter, so only the 8-wave tall path takes one
+  GemmParams pd = p;
+  const bool tall = UseTall(&pd, stream, /*dry=*/true);
   if (tall && UseTallPipe(p0, a.nonzeros / (kBlock * kBlock),
                           ((long long)a.cols + kBlock - 1) / kBlock, ta, tb)) {
     GemmParams q = p0;
@@ -1084,6 +1099,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     q.num_tiles = hipGetDevice(&dev) == hipSuccess ? DeviceCUs(dev) : 0;
     return LaunchDsd4w(dtype, q, 7, false, stream, false, false);
   }
+  if (tall) (void)UseTall(&p, stream);
   if (Dsd4wEnabled() &&
       Dsd4wApplies(p, Dsd4wForced() ? (1LL << 40) : a.nonzeros / (kBlock * kBlock),
                    !ta, tb, false, tall)) {
@@ -1415,6 +1431,47 @@ int SddPlan(const void *a, bool ta, const void *b, bool tb, const void *c) {
     return -1;
   if (UseGroupedSdd(&p, cm, tb)) return 1;
   return PrepareSddKsplit(&p, cm, ta, tb, nullptr, /*dry=*/true) ? 2 : 0;
+}
+
+// The kernel behind SddPlan's tile plan (what RunSdd launches): 0 the
+// 8-wave k-split 128 x 128 block tile, 1 grouped tiles on the 8-wave
+// kernel, 2 the 4-wave K-split, 3 grouped tiles on the 4-wave kernel, -1
+// rejected.
+int SddKernel(const void *a, bool ta, const void *b, bool tb, const void *c) {
+  const int plan = SddPlan(a, ta, b, tb, c);
+  if (plan != 1) return plan;
+  GemmParams p;
+  const BlockMatrix &cm = *static_cast<const BlockMatrix *>(c);
+  if (PrepareSdd(*static_cast<const Matrix *>(a), ta,
+                 *static_cast<const Matrix *>(b), tb, cm, &p) != Status::kOk ||
+      !UseGroupedSdd(&p, cm, tb))
+    return -1;
+  return Dsd4wEnabled() && Sdd4wApplies(p, true, ta, tb, cm.nonzeros / (kBlock * kBlock))
+             ? 3
+             : 1;
+}
+
+// Which kernel RunDds would launch on `stream` (no launch, nothing
+// allocated): 0 the 8-wave 128 x 512 tile, 1 the 4-wave kernel, 2 the tall
+// configuration, 3 split mode on the 8-wave kernel, -1 rejected.
+int DdsPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
+            hipStream_t stream) {
+  if (!a || !b || !c) return -1;
+  GemmParams p;
+  bool needs_meta = false;
+  const BlockMatrix &bm = *static_cast<const BlockMatrix *>(b);
+  if (PrepareDds(*static_cast<const Matrix *>(a), ta, bm, tb,
+                 *static_cast<const Matrix *>(c), &p, &needs_meta) != Status::kOk)
+    return -1;
+  PreparePairs(&p, bm.nonzeros / (kBlock * kBlock), stream, /*dry=*/true);
+  const bool tall = UseTall(&p, stream, /*dry=*/true);
+  if (Dsd4wEnabled() &&
+      Dds4wApplies(p, Dsd4wForced() ? (1LL << 40) : bm.nonzeros / (kBlock * kBlock), tb,
+                   !ta, true, tall))
+    return 1;
+  if (tall) return 2;
+  if (p.pair != 0 && p.pair_split > 1) return 3;
+  return 0;
 }
 
 // Which kernel RunDsd would launch for this problem on `stream` (no

@@ -168,7 +168,7 @@ def test_tuning_knobs_host_only():
     defaults = {"pairs": 1, "pair_xcd2": 3, "split": 1, "split_min_bn": 128,
                 "dsd4w": 1, "grouped_sdd": 1, "grouped_min_per_cu": 4,
                 "tall": 1, "tall_persistent": 1, "dds_xcd2": 3,
-                "sdd4w_max_ld": 16384, "pair_fault": 0, "sdd_ksplit": 8,
+                "sdd4w_max_ld": 16384, "pair_fault": 0, "sdd_ksplit": 1,
                 "sdd_ksplit_min_k": 6144, "sdd_order": 1, "tall4w": 1,
                 "tall_flush_w": 4, "tall_odd_share": 120}
     for name, v in defaults.items():

@@ -9,8 +9,10 @@ hide them:
   config 5  DSD M=131072 K=N=4096 2%, and its row-panel split
 
 Full-size launches. Configs 2 and 3: every output element against the CPU
-oracle (oracle/). Configs 4 and 5: sampled block-rows / blocks, and
-size-independent properties (exact zeros of empty rows, bit-identical
+oracle (oracle/). Config 4: every output block / row-block through float64
+linearity checksums (row sums against the operands), plus every expert's
+first and last block-row against the oracle. Config 5: sampled block-rows,
+and size-independent properties (exact zeros of empty rows, bit-identical
 sharded results) cover the rest. Tolerance as
 tests/helpers.py (1e-2 relative fp16, 2e-2 bf16). Config 1 is the host
 reference alone (tests/test_oracle.py, bench.py's config-1 line).
@@ -101,20 +103,31 @@ def test_sdd_dds_pair_config3_full():
                        "f16", f"dds row-block {r}")
 
 
-def test_moe_config4_bf16_sampled():
-    """BASELINE config 4 at full size (8 experts, 8192 tokens, d_model 4096,
-    d_ff 14336, bf16, expert block-diagonal topology): SDD h = x.w1 at the
-    expert blocks, then DSD y = h.w2. Sampled blocks / row-blocks against the
-    oracle; host operands are drawn on the device and only the slices the
-    oracle needs come back."""
+def _moe_setup(seed):
     E, T, DM, FF = 8, 8192, 4096, 14336
     cols = E * FF
     rpe, cpe = T // E // 128, FF // 128
     off, idx = mu.expert_block_diagonal(E, rpe, cpe)
-    nb = int(off[-1])
     g = torch.Generator(device="cuda")
-    g.manual_seed(4)
+    g.manual_seed(seed)
     rnd = lambda *s: (torch.rand(*s, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
+    return E, T, DM, FF, cols, rpe, cpe, off, idx, rnd
+
+
+def _f64(t):
+    return t.double().cpu().numpy()
+
+
+def test_moe_config4_bf16_all_blocks():
+    """BASELINE config 4 at full size (8 experts, 8192 tokens, d_model 4096,
+    d_ff 14336, bf16, expert block-diagonal topology): SDD h = x.w1 at the
+    expert blocks, then DSD y = h.w2.
+      * all 7168 SDD blocks: row sums of h_b = x_r . (w1_c . 1);
+      * all 64 DSD row-blocks: y . 1 = h . (w2 . 1);
+      * every expert's first and last block-row of h (all its 112 blocks)
+        and of y element by element against the oracle."""
+    E, T, DM, FF, cols, rpe, cpe, off, idx, rnd = _moe_setup(4)
+    nb = int(off[-1])
     x, w1, w2 = rnd(T, DM), rnd(DM, cols), rnd(cols, DM)
     hv = torch.full((nb, 128, 128), float("nan"), dtype=torch.bfloat16, device="cuda")
     Hm = sp.BlockMatrix(T, cols, 128, nb * 16384, hv,
@@ -126,38 +139,50 @@ def test_moe_config4_bf16_sampled():
     sp.Matmul(sp.Matrix(T, DM, x), False, sp.Matrix(DM, cols, w1), False, Hm)
     sp.Matmul(Hm, False, sp.Matrix(cols, DM, w2), False, sp.Matrix(T, DM, y))
     _sync()
-    f = lambda t: t.float().cpu().numpy()
+    assert sp.pair_errors() == 0
     rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
-    for b in (0, 1000, nb // 2 + 37, nb - 1):
-        r, c = int(rows[b]), int(idx[b])
-        ref = O.gemm(f(x[r * 128:(r + 1) * 128]), False,
-                     f(w1[:, c * 128:(c + 1) * 128]), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(hv[b]), ref, "bf16", f"moe sdd block {b}")
-    for r in (0, 29, 63):
-        e = r // rpe
-        h_row = f(hv[off[r]:off[r + 1]]).transpose(1, 0, 2).reshape(128, FF)
-        ref = O.gemm(h_row, False, f(w2[e * FF:(e + 1) * FF]), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(y[r * 128:(r + 1) * 128]), ref, "bf16",
-                       f"moe dsd row-block {r}")
+    # SDD checksum over every block: x (T x DM) . s1 (DM x cols/128), s1 the
+    # per-block-column sums of w1
+    x64 = _f64(x)
+    s1 = _f64(w1).reshape(DM, cols // 128, 128).sum(axis=2)
+    xs = x64 @ s1                                          # [T][cols/128]
+    h32 = hv.float().cpu().numpy()                         # [nb][128][128]
+    expect = xs.reshape(T // 128, 128, cols // 128)[rows, :, idx]   # [nb][128]
+    H.rowsum_check(h32, expect, 2, "moe sdd")
+    # DSD checksum over every row-block: y . 1 = sum_b h_b . v_c, v = w2 . 1
+    v = _f64(w2).sum(axis=1).reshape(cols // 128, 128)
+    hb = np.einsum("bij,bj->bi", h32.astype(np.float64), v[idx])    # [nb][128]
+    ey = np.zeros((T // 128, 128))
+    np.add.at(ey, rows, hb)
+    y32 = y.float().cpu().numpy()
+    H.rowsum_check(y32, ey.reshape(T), 1, "moe dsd")
+    # every expert's first and last block-row against the oracle
+    for e in range(E):
+        for r in (e * rpe, (e + 1) * rpe - 1):
+            c0 = e * cpe
+            ref = O.gemm(x[r * 128:(r + 1) * 128].float().cpu().numpy(), False,
+                         w1[:, c0 * 128:(c0 + cpe) * 128].float().cpu().numpy(),
+                         False, threads=H.oracle_threads())
+            got = h32[off[r]:off[r + 1]].transpose(1, 0, 2).reshape(128, FF)
+            assert (idx[off[r]:off[r + 1]] == np.arange(c0, c0 + cpe)).all()
+            H.assert_close(got, ref, "bf16", f"moe sdd block-row {r}")
+            ref = O.gemm(got, False, w2[e * FF:(e + 1) * FF].float().cpu().numpy(),
+                         False, threads=H.oracle_threads())
+            H.assert_close(y32[r * 128:(r + 1) * 128], ref, "bf16",
+                           f"moe dsd row-block {r}")
 
 
-def test_moe_config4_backward_bf16_sampled():
-    """The MegaBlocks backward of config 4's second layer at full size (8
-    experts, 8192 tokens, d_model 4096, d_ff 14336, bf16):
+def test_moe_config4_backward_bf16_all_blocks():
+    """The MegaBlocks backward of config 4's second layer at full size:
       dW2 = h^T . dy   (DSD TN: h^T has 896 block-rows, the tall path, with
                         h's transposed metadata built on the device),
       dh  = dy . W2^T  at h's blocks (SDD NT).
-    Sampled row-blocks / blocks against the oracle."""
-    E, T, DM, FF = 8, 8192, 4096, 14336
-    cols = E * FF
-    rpe, cpe = T // E // 128, FF // 128
-    off, idx = mu.expert_block_diagonal(E, rpe, cpe)
+    Every output covered: dW2 . 1 = h^T . (dy . 1) over all 896 row-blocks,
+    and the row sums of all 7168 dh blocks = dy_r . (W2_c^T . 1); every
+    expert's first and last dW2 row-block and dh block-row against the
+    oracle."""
+    E, T, DM, FF, cols, rpe, cpe, off, idx, rnd = _moe_setup(44)
     nb = int(off[-1])
-    g = torch.Generator(device="cuda")
-    g.manual_seed(44)
-    rnd = lambda *s: (torch.rand(*s, generator=g, device="cuda") * 2 - 1).to(torch.bfloat16)
     hv, dy, w2 = rnd(nb, 128, 128), rnd(T, DM), rnd(cols, DM)
     mk = lambda vals: sp.BlockMatrix(T, cols, 128, nb * 16384, vals,
                                      torch.from_numpy(off).cuda(),
@@ -173,27 +198,40 @@ def test_moe_config4_backward_bf16_sampled():
     sp.RowIndices(dHm, dHm.row_indices)
     sp.Matmul(sp.Matrix(T, DM, dy), False, sp.Matrix(cols, DM, w2), True, dHm)
     _sync()
-    f = lambda t: t.float().cpu().numpy()
-    # dW2 row-block c (= h's block-column c, expert e = c // cpe): only the
-    # expert's tokens hold h blocks in that column.
+    assert sp.pair_errors() == 0
     rows = np.repeat(np.arange(len(off) - 1), np.diff(off))
-    for c in (0, 111, 500, cols // 128 - 1):
-        e = c // cpe
+    h32 = hv.float().cpu().numpy()
+    dy64 = _f64(dy)
+    # dW2 . 1 = h^T . u, u = dy . 1: block b adds h_b^T . u_r to row-block c
+    u = dy64.sum(axis=1).reshape(T // 128, 128)
+    cb = np.einsum("bij,bi->bj", h32.astype(np.float64), u[rows])   # [nb][128]
+    ew = np.zeros((cols // 128, 128))
+    np.add.at(ew, idx, cb)
+    w32 = dw2.float().cpu().numpy()
+    H.rowsum_check(w32, ew.reshape(cols), 1, "moe bwd dW2")
+    # dh_b row sums = dy_r . s_c, s_c = sum of W2's rows in block c
+    s = _f64(w2).reshape(cols // 128, 128, DM).sum(axis=1)        # [cols/128][DM]
+    ds = dy64 @ s.T                                               # [T][cols/128]
+    expect = ds.reshape(T // 128, 128, cols // 128)[rows, :, idx]
+    d32 = dhv.float().cpu().numpy()
+    H.rowsum_check(d32, expect, 2, "moe bwd dh")
+    # every expert's first and last row-block / block-row against the oracle
+    for e in range(E):
         t0, t1 = e * rpe * 128, (e + 1) * rpe * 128
-        hcol = np.concatenate([f(hv[b]) for b in range(nb)
-                               if idx[b] == c and t0 <= rows[b] * 128 < t1])
-        assert hcol.shape == (t1 - t0, 128)
-        ref = O.gemm(hcol.T.copy(), False, f(dy[t0:t1]), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(dw2[c * 128:(c + 1) * 128]), ref, "bf16",
-                       f"moe bwd dW2 row-block {c}")
-    for b in (0, 777, nb // 2 + 5, nb - 1):
-        r, c = int(rows[b]), int(idx[b])
-        ref = O.gemm(f(dy[r * 128:(r + 1) * 128]), False,
-                     f(w2[c * 128:(c + 1) * 128]).T.copy(), False,
-                     threads=H.oracle_threads())
-        H.assert_close(f(dhv[b]), ref, "bf16", f"moe bwd dh block {b}")
-    assert not torch.isnan(dw2.float()).any()
+        for c in (e * cpe, (e + 1) * cpe - 1):
+            hcol = np.concatenate([h32[b] for b in range(off[e * rpe], off[(e + 1) * rpe])
+                                   if idx[b] == c])
+            assert hcol.shape == (t1 - t0, 128)
+            ref = O.gemm(hcol.T.copy(), False, dy[t0:t1].float().cpu().numpy(),
+                         False, threads=H.oracle_threads())
+            H.assert_close(w32[c * 128:(c + 1) * 128], ref, "bf16",
+                           f"moe bwd dW2 row-block {c}")
+        for r in (e * rpe, (e + 1) * rpe - 1):
+            ref = O.gemm(dy[r * 128:(r + 1) * 128].float().cpu().numpy(), False,
+                         w2[e * FF:(e + 1) * FF].float().cpu().numpy(), True,
+                         threads=H.oracle_threads())
+            got = d32[off[r]:off[r + 1]].transpose(1, 0, 2).reshape(128, FF)
+            H.assert_close(got, ref, "bf16", f"moe bwd dh block-row {r}")
 
 
 def test_tall_panel_config5_sampled():

@@ -377,11 +377,14 @@ KSPLIT_CASES = [
 
 @pytest.fixture
 def ksplit_any_k():
-    """The K-split for every K >= 512 (default: K >= 6144, knob
-    sdd_ksplit_min_k), so these small problems take it."""
+    """The K-split on (off by default: knob sdd_ksplit = 1) for every K >=
+    512 (default gate: K >= 6144, knob sdd_ksplit_min_k), so these small
+    problems take it."""
+    prev_s = sp.tuning("sdd_ksplit", 8)
     prev = sp.tuning("sdd_ksplit_min_k", 512)
     yield
     sp.tuning("sdd_ksplit_min_k", prev)
+    sp.tuning("sdd_ksplit", prev_s)
 
 
 @pytest.mark.parametrize("m,k,n,nb,dtype", KSPLIT_CASES)
@@ -511,13 +514,24 @@ def test_graph_capture_sdd_ksplit(ksplit_any_k):
 
 
 def test_sdd_plan_ksplit_default_gate():
-    """Default gate: 205 blocks of 4096^2 take the 8-wave k-split tile at
-    K = 4096 and the K-split grouped tiles at K = 8192 (exact there too)."""
-    for k, want in ((4096, 0), (8192, 2)):
+    """The K-split is off by default (its all-to-all chunk wait
+    needs the whole grid resident): 205 blocks of 4096^2 take the 8-wave
+    k-split tile at K = 4096 and 8192. Opted in (knob sdd_ksplit = 8), the
+    K = 6144 gate still keeps K = 4096 off it and takes K = 8192 (exact)."""
+    for k in (4096, 8192):
         got, exp, plan = kat_sdd(4096, k, 4096, None, False, False, "f16", nb=205,
                                  seed=k)
-        assert plan == want, (k, plan)
+        assert plan == 0, (k, plan)
         _equal(got, exp, f"sdd 205 blocks k={k}")
+    prev = sp.tuning("sdd_ksplit", 8)
+    try:
+        for k, want in ((4096, 0), (8192, 2)):
+            got, exp, plan = kat_sdd(4096, k, 4096, None, False, False, "f16",
+                                     nb=205, seed=k)
+            assert plan == want, (k, plan)
+            _equal(got, exp, f"sdd 205 blocks k={k} (K-split on)")
+    finally:
+        sp.tuning("sdd_ksplit", prev)
     assert sp.pair_errors() == 0
 
 
@@ -716,7 +730,7 @@ def test_graph_capture_with_pairs():
 
 
 def test_graph_capture_workspace_freed_with_graph():
-    """A capture's pair workspace (32 MiB) and persistent counter live as long
+    """A capture's pair workspace (64 MiB) and persistent counter live as long
     as the captured graph: destroying the graph and its executable releases
     them (a user object retained by the graph, dispatch.cpp
     TieToCapturedGraph), so re-capturing per shape does not pin memory or
@@ -759,7 +773,7 @@ def test_graph_capture_reuses_released_workspace():
     """Repeated capture / replay / destroy with no eager launch and no
     sputnik_capture_workspaces() call in between: each new
     capture re-ties the released workspace of the destroyed graph instead of
-    allocating another 32 MiB (device memory stays flat), replays stay
+    allocating another 64 MiB (device memory stays flat), replays stay
     bit-exact, and sputnik_capture_workspaces() finally frees it."""
     import time
     got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, 0.5, False, False,
