@@ -1,5 +1,7 @@
-"""Same-process A/B of one tuning knob on one bench workload problem:
+"""Same-process A/B of tuning knobs on one bench workload problem:
 python scripts/exp_knob_ab.py KNOB v1,v2,... [--workload panel|dsd] [--density D]
+Several knobs at once: KNOB1+KNOB2 with values a1:a2,b1:b2,... (one setting
+per comma, the knobs' values joined by ':').
 Interleaved rounds, median per value (us)."""
 import argparse
 import json
@@ -24,7 +26,10 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=30)
     a = ap.parse_args()
-    vals = [int(v) for v in a.values.split(",")]
+    knobs = a.knob.split("+")
+    vals = a.values.split(",")
+    setting = {v: [int(x) for x in v.split(":")] for v in vals}
+    assert all(len(x) == len(knobs) for x in setting.values()), "one value per knob"
     dev = torch.device("cuda", 0)
     args = types.SimpleNamespace(seed=0, k=4096, n=4096, m=4096, dtype="f16")
     if a.workload == "panel":
@@ -46,11 +51,12 @@ def main():
     else:
         prob = bench.dsd_panel(args, 1, 0, dev, a.density, m_total=4096)
     res = {v: [] for v in vals}
-    prev = sp.tuning(a.knob)
+    prev = [sp.tuning(k) for k in knobs]
     try:
         for _ in range(a.rounds):
             for v in vals:
-                sp.tuning(a.knob, v)
+                for k, x in zip(knobs, setting[v]):
+                    sp.tuning(k, x)
                 fn = prob.launcher()
                 for _ in range(5):
                     fn()
@@ -63,8 +69,9 @@ def main():
                 torch.cuda.synchronize()
                 res[v].append(s.elapsed_time(e) * 1e3 / a.iters)
     finally:
-        sp.tuning(a.knob, prev)
-    out = {"knob": a.knob, "workload": a.workload,
+        for k, x in zip(knobs, prev):
+            sp.tuning(k, x)
+    out = {"knob": a.knob, "workload": a.workload, "density": a.density,
            "us_median": {v: round(sorted(x)[len(x) // 2], 2) for v, x in res.items()},
            "us_min": {v: round(min(x), 2) for v, x in res.items()}}
     print(json.dumps(out), flush=True)

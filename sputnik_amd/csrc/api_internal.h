@@ -100,6 +100,7 @@ enum KnobId {
   kKnobTall4w,
   kKnobTallFlushW,
   kKnobTallOddShare,
+  kKnobMinHandoff,
   kNumKnobs
 };
 int Knob(KnobId k);

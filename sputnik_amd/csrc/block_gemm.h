@@ -212,6 +212,9 @@ struct GemmParams {
   // quarter blocks (the cost-balanced cut of the block sequence).
   int tall_flush_w;
   int tall_odd_share;  // ... and an odd XCD's workgroup share, percent of an even one's
+  // 4-wave pair launches: the smallest hand-off (blocks) a pair makes;
+  // below it the heavy row keeps its blocks (0: SPUTNIK_MIN_HANDOFF).
+  int min_handoff;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

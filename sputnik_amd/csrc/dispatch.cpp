@@ -119,6 +119,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"tall4w", "SPUTNIK_AMD_TALL4W", 1, 0, 1},
     {"tall_flush_w", "SPUTNIK_AMD_TALL_FLUSH_W", 4, 0, 64},
     {"tall_odd_share", "SPUTNIK_AMD_TALL_ODD_SHARE", 120, 50, 200},
+    {"min_handoff", "SPUTNIK_AMD_MIN_HANDOFF", 2, 1, 64},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -417,6 +418,7 @@ static void PreparePairs(GemmParams *p, long long blocks, hipStream_t stream,
   // the pairs (r04d: +0.5% at 50%).
   const int xcd2 = Knob(kKnobPairXcd2);
   p->pair_xcd2 = xcd2 != 0 && blocks >= 8LL * p->num_rows ? xcd2 : 0;
+  p->min_handoff = Knob(kKnobMinHandoff);
   // Split mode (GemmParams::pair_split) when the tiles fill at most half of
   // the workgroup slots (e.g. 512-2048-row panels of a strong-scaled 4096^2,
   // or narrow N) and the rows hold at least 4 blocks on average: two

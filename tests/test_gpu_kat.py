@@ -208,6 +208,38 @@ def test_kat_dsd_4096_pairs(ta):
     assert sp.pair_errors() == 0
 
 
+@pytest.fixture(params=[1, 3], ids=["handoff1", "handoff3"])
+def pair_placement(request):
+    """Smallest pair hand-off (knob min_handoff, default 2), restored after."""
+    prev = sp.tuning("min_handoff", request.param)
+    yield request.param
+    sp.tuning("min_handoff", prev)
+
+
+@pytest.mark.parametrize("density", [0.1, 0.3, 0.5, 0.9])
+@pytest.mark.parametrize("op", ["dsd", "dds"])
+def test_kat_4096_pair_placement(op, density, pair_placement):
+    """4096^3 pair launches with 1-block hand-offs allowed, or only from 3
+    blocks: every split point is still exact (integer operands), no
+    hand-off times out, and a second launch agrees bit for bit."""
+    seed = int(density * 100) + 17
+    if op == "dsd":
+        got, want, (A, Bd, C) = kat_dsd(4096, 4096, 4096, density, False, False,
+                                        "f16", seed=seed)
+        _equal(got, want, f"dsd 4096 {density} {pair_placement}")
+        first = got.clone()
+        sp.Matmul(A.m, False, Bd.m, False, C)
+    else:
+        got, want, (A, Bs, C) = kat_dds(4096, 4096, 4096, density, False, False,
+                                        "f16", seed=seed, handles=True)
+        _equal(got, want, f"dds 4096 {density} {pair_placement}")
+        first = got.clone()
+        sp.Matmul(A.m, False, Bs.m, False, C)
+    torch.cuda.synchronize()
+    assert torch.equal(first, got)
+    assert sp.pair_errors() == 0
+
+
 @pytest.mark.parametrize("m", [512, 1024, 2048])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False),
                                    (False, True), (True, True)])
@@ -743,6 +775,15 @@ def test_graph_capture_workspace_freed_with_graph():
     Td = IDense(256, 512, rng, "f16")
     CT, gotT = _nan_out(65536, 512, "f16")
     torch.cuda.synchronize()
+    prev = sp.tuning("tall4w", 0)  # the 8-wave persistent tall path: a counter
+    try:
+        _capture_release_cycle(A, Bd, C, got, want, T, Td, CT)
+    finally:
+        sp.tuning("tall4w", prev)
+
+
+def _capture_release_cycle(A, Bd, C, got, want, T, Td, CT):
+    import time
     base = sp.capture_workspaces()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -860,11 +901,50 @@ def test_graph_capture_tall_persistent():
     counter already exists: the captured launch gets a counter pair of its
     own capture (the kernel leaves it at zero), so replays interleaved with
     eager persistent launches on the same stream all stay exact."""
+    prev = sp.tuning("tall4w", 0)  # the 8-wave persistent tall path
+    try:
+        _tall_persistent_capture()
+    finally:
+        sp.tuning("tall4w", prev)
+
+
+def test_graph_capture_tall_pipe_takes_no_counter():
+    """The tall DSD NN pipeline (4-wave, plan 4) needs no persistent tile
+    counter: a captured tall-pipe launch ties no capture workspace (ADVICE
+    r05: the tall decision is made dry before the counter is allocated),
+    and its replays are exact."""
+    rng = np.random.default_rng(13)
+    A = ISparse(65536, 256, 0.3, rng, "f16")
+    Bd = IDense(256, 512, rng, "f16")
+    want = _expect(A.dense.astype(np.float64) @ Bd.values, "f16")
+    C, got = _nan_out(65536, 512, "f16")
+    prev = sp.tuning("tall4w", 1)
+    try:
+        assert sp.dsd_plan(A.m, False, Bd.m, False, C) == 4
+        torch.cuda.synchronize()
+        before = sp.capture_workspaces()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            sp.MatmulEx(A.m, False, Bd.m, False, C)
+        assert sp.capture_workspaces() == before, "tall pipe tied a workspace"
+        for _ in range(2):
+            got.fill_(float("nan"))
+            g.replay()
+            _equal(got, want, "tall pipe replay")
+        del g
+    finally:
+        sp.tuning("tall4w", prev)
+
+
+def _tall_persistent_capture():
     rng = np.random.default_rng(12)
     A = ISparse(65536, 256, 0.3, rng, "f16")
     Bd = IDense(256, 512, rng, "f16")
     want = _expect(A.dense.astype(np.float64) @ Bd.values, "f16")
     C, got = _nan_out(65536, 512, "f16")
+    assert sp.dsd_plan(A.m, False, Bd.m, False, C) == 2
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
