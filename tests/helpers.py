@@ -109,25 +109,25 @@ def empty_dense(rows, cols, dtype="f16", device="cuda", fill=float("nan")):
 # Linearity checksums (tests/test_gpu_configs.py config 4): row sums of a
 # full-size output against exact float64 sums computed from the operands.
 #
-# Checksum tolerance: the outputs are bf16 (8 significant bits), so each
-# element carries a round-to-nearest error e with |e| <= 2^-8 |y|, zero mean,
-# variance <= (2^-8 y)^2 / 3; a row sum of n of them is off from the exact
-# sum by about 2^-8 sqrt(sum y^2 / 3). The bound is 8 of those (the fp32
-# accumulation error is orders of magnitude smaller). One missing or wrong
-# 128-long contribution (a dropped block, a wrong k-block) moves a row sum by
-# 10-40x that bound at these shapes. The launches are deterministic, so the
-# check cannot flake on a fixed seed.
-_BF16_U = 2.0 ** -8
+# Checksum tolerance: an output of p significant bits (bf16 8, fp16 11)
+# carries a round-to-nearest error e per element with |e| <= 2^-p |y|, zero
+# mean, variance <= (2^-p y)^2 / 3; a row sum of n of them is off from the
+# exact sum by about 2^-p sqrt(sum y^2 / 3). The bound is 8 of those (the
+# fp32 accumulation error is orders of magnitude smaller). One missing or
+# wrong 128-long contribution (a dropped block, a wrong k-block) moves a row
+# sum by 10-40x that bound at these shapes. The launches are deterministic,
+# so the check cannot flake on a fixed seed.
+_ROUND_U = {"bf16": 2.0 ** -8, "f16": 2.0 ** -11}
 
 
-def rowsum_check(y, expect, axis, what):
-    """y: the bf16 output as float32; expect: exact float64 sums of y along
-    `axis` computed from the operands."""
+def rowsum_check(y, expect, axis, what, dtype="bf16"):
+    """y: the output (bf16 / fp16) as float32; expect: exact float64 sums of
+    y along `axis` computed from the operands."""
     assert np.isfinite(y).all(), f"{what}: non-finite output"
     got = y.sum(axis=axis, dtype=np.float64)
     sq = np.square(y, dtype=np.float64).sum(axis=axis)
     rms = float(np.sqrt(np.mean(expect * expect)))
-    tol = 8 * _BF16_U * np.sqrt(sq / 3) + 1e-6 * rms
+    tol = 8 * _ROUND_U[dtype] * np.sqrt(sq / 3) + 1e-6 * rms
     err = np.abs(got - expect)
     bad = err > tol
     assert not bad.any(), (

@@ -11,9 +11,10 @@ hide them:
 Full-size launches. Configs 2 and 3: every output element against the CPU
 oracle (oracle/). Config 4: every output block / row-block through float64
 linearity checksums (row sums against the operands), plus every expert's
-first and last block-row against the oracle. Config 5: sampled block-rows,
-and size-independent properties (exact zeros of empty rows, bit-identical
-sharded results) cover the rest. Tolerance as
+first and last block-row against the oracle. Config 5: every row through
+the same checksum, sampled block-rows against the oracle, and
+size-independent properties (exact zeros of empty rows, bit-identical
+sharded results). Tolerance as
 tests/helpers.py (1e-2 relative fp16, 2e-2 bf16). Config 1 is the host
 reference alone (tests/test_oracle.py, bench.py's config-1 line).
 """
@@ -236,7 +237,8 @@ def test_moe_config4_backward_bf16_all_blocks():
 
 def test_tall_panel_config5_sampled():
     """BASELINE config 5 at full size on one device: DSD M=131072, K=N=4096,
-    2% density (656 blocks over 1024 block-rows, most rows empty). Empty
+    2% density (656 blocks over 1024 block-rows, most rows empty). Every
+    row's sum against the float64 linearity checksum C.1 = A.(B.1); empty
     block-rows must be exact zeros; sampled non-empty rows against the
     oracle; and the per-rank row-panel split (shard_rows_by_nnz) run as
     separate calls reproduces the single-call result bit-exactly."""
@@ -248,6 +250,13 @@ def test_tall_panel_config5_sampled():
     C, c_t = H.empty_dense(M, 4096)
     sp.Matmul(A.matrix, False, B.matrix, False, C)
     _sync()
+    # every row: C . 1 = A . (B . 1), float64 from the operands
+    v = B.values.astype(np.float64).sum(axis=1).reshape(32, 128)
+    rows_of = np.repeat(np.arange(M // 128), np.diff(A.offsets))
+    contrib = np.einsum("bij,bj->bi", A.values.astype(np.float64), v[A.indices])
+    expect = np.zeros((M // 128, 128))
+    np.add.at(expect, rows_of, contrib)
+    H.rowsum_check(c_t.float().cpu().numpy(), expect.reshape(M), 1, "panel", "f16")
     counts = np.diff(A.offsets)
     empty = np.nonzero(counts == 0)[0]
     assert len(empty) > 0

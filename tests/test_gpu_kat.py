@@ -567,6 +567,33 @@ def test_sdd_plan_ksplit_default_gate():
     assert sp.pair_errors() == 0
 
 
+def test_kernel_queries_match_config3():
+    """sputnik_sdd_kernel / sputnik_dds_plan (what bench.py labels its lines
+    with) at config 3's shapes: 205 SDD blocks of 4096^2 at K = 4096 take
+    the 8-wave k-split block tile (0), the DDS g . C the 4-wave kernel (1);
+    from 4 blocks per CU the SDD takes the 4-wave grouped tiles (3)."""
+    rng = np.random.default_rng(21)
+    A = IDense(4096, 4096, rng, "f16")
+    Bd = IDense(4096, 4096, rng, "f16")
+    Cs = ISparse(4096, 4096, None, rng, "f16", nb=205)
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    assert sp.sdd_plan(A.m, False, Bd.m, False, Cs.m) == 0
+    assert sp.sdd_kernel(A.m, False, Bd.m, False, Cs.m) == 0
+    out, _ = _nan_out(4096, 4096, "f16")
+    assert sp.dds_plan(A.m, False, Cs.m, False, out) == 1
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    Cg = ISparse(4096, 4096, None, rng, "f16", nb=4 * cus)
+    sp.AllocateRowIndicesBuffer(Cg.m)
+    assert sp.sdd_plan(A.m, False, Bd.m, False, Cg.m) == 1
+    assert sp.sdd_kernel(A.m, False, Bd.m, False, Cg.m) == 3
+    prev = sp.select_dsd_kernel(0)  # the 8-wave kernel everywhere
+    try:
+        assert sp.sdd_kernel(A.m, False, Bd.m, False, Cg.m) == 1
+        assert sp.dds_plan(A.m, False, Cs.m, False, out) == 0
+    finally:
+        sp.select_dsd_kernel(prev)
+
+
 def test_sdd_plan_threshold():
     """Just below 4 blocks per CU the k-split block tile is chosen, from 4
     the grouped one (dispatch.cpp UseGroupedSdd)."""
