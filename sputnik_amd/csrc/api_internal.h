@@ -101,6 +101,7 @@ enum KnobId {
   kKnobTallFlushW,
   kKnobTallOddShare,
   kKnobMinHandoff,
+  kKnobXcdRows,
   kNumKnobs
 };
 int Knob(KnobId k);

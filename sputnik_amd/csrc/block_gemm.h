@@ -215,6 +215,10 @@ struct GemmParams {
   // 4-wave pair launches: the smallest hand-off (blocks) a pair makes;
   // below it the heavy row keeps its blocks (0: SPUTNIK_MIN_HANDOFF).
   int min_handoff;
+  // 4-wave plain launches with 64..kLptRows rows of equal count, R % 8 == 0:
+  // XCD x takes a contiguous eighth of the rows over every panel
+  // (dsd4w.hip; 0: the panel-major XCD map).
+  int xcd_rows;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

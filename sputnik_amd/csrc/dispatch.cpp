@@ -120,6 +120,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"tall_flush_w", "SPUTNIK_AMD_TALL_FLUSH_W", 4, 0, 64},
     {"tall_odd_share", "SPUTNIK_AMD_TALL_ODD_SHARE", 120, 50, 200},
     {"min_handoff", "SPUTNIK_AMD_MIN_HANDOFF", 2, 1, 64},
+    {"xcd_rows", "SPUTNIK_AMD_XCD_ROWS", 1, 0, 1},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1084,6 +1085,7 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
+  p.xcd_rows = Knob(kKnobXcdRows);
   PreparePairs(&p, a.nonzeros / (kBlock * kBlock), stream);
   const GemmParams p0 = p;  // (before the tall configuration)
   // decide without allocating first: the tall pipeline needs no persistent
@@ -1130,6 +1132,7 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
     if (e != hipSuccess) return e;
   }
   p.debug = g_debug;
+  p.xcd_rows = Knob(kKnobXcdRows);
   PreparePairs(&p, b.nonzeros / (kBlock * kBlock), stream);
   const bool tall = UseTall(&p, stream);
   if (Dsd4wEnabled() &&

@@ -240,6 +240,31 @@ def test_kat_4096_pair_placement(op, density, pair_placement):
     assert sp.pair_errors() == 0
 
 
+@pytest.mark.parametrize("op", ["dsd", "dds"])
+@pytest.mark.parametrize("n", [4096, 2048])
+def test_kat_uniform_rows_xcd_map(op, n):
+    """Plain 4-wave launches over 64 rows of equal count (an expert-diagonal
+    topology, as MegaBlocks' h . w2): the XCD-row tile map (knob xcd_rows,
+    dsd4w.hip) gives every tile to exactly one workgroup -- exact, and bit-
+    identical to the panel-major map."""
+    topo = mu.expert_block_diagonal(8, 8, 8)   # 64 x 64 blocks, 8 per row / column
+    outs = []
+    for xr in (1, 0):
+        prev = sp.tuning("xcd_rows", xr)
+        try:
+            if op == "dsd":
+                got, want, _ = kat_dsd(8192, 8192, n, None, False, False, "f16",
+                                       seed=31, topology=topo)
+            else:
+                got, want = kat_dds(n, 8192, 8192, None, False, False, "f16",
+                                    seed=31, topology=topo)
+        finally:
+            sp.tuning("xcd_rows", prev)
+        _equal(got, want, f"{op} uniform rows n={n} xcd_rows={xr}")
+        outs.append(got.clone())
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("m", [512, 1024, 2048])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False),
                                    (False, True), (True, True)])
