@@ -28,6 +28,7 @@ def main():
     # --op op: one product of bench.OpProblem (square dims = --k), MatmulEx.
     ap.add_argument("--xop", default="dsd", choices=["dsd", "dds", "sdd"])
     ap.add_argument("--trans", default="NN")
+    ap.add_argument("--topo-seed", type=int, default=0)
     args = ap.parse_args()
     import torch
     import bench
@@ -64,9 +65,11 @@ def main():
         import numpy as np
         from sputnik_amd import matrix_utils as mu
         nz = mu.nonzeros_for_density(args.m, args.k, args.density)
+        # (--topo-seed: bench.py dsd_panel's shared seed is 7919 s + seed_off,
+        # 5 for config 5)
         off, idx = mu.random_topology(args.m // 128, args.k // 128,
                                       nz // (128 * 128),
-                                      np.random.default_rng(0))
+                                      np.random.default_rng(args.topo_seed))
         prob = bench.DsdProblem(args.m, args.k, off, idx, args.n, False,
                                 False, args.dtype, 0, dev)
         ca, cb, cc = prob.A._c(), prob.B._c(), prob.C._c()

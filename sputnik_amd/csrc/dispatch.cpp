@@ -195,18 +195,28 @@ static int CaptureState(hipStream_t stream, unsigned long long *id) {
 // being captured: the thread switches to relaxed capture mode (hipMalloc is
 // not a stream operation), and the fill runs on a private non-blocking
 // stream that no capture touches, synchronized before returning.
+// The library's private non-blocking stream of a device (created on first
+// use, kept for the process; caller holds g_pairs_mu).
+static hipStream_t g_side[kMaxDevices] = {};
+static hipError_t SideStream(int dev, hipStream_t *out) {
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  if (g_side[dev] == nullptr) {
+    const hipError_t e = hipStreamCreateWithFlags(&g_side[dev], hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  *out = g_side[dev];
+  return hipSuccess;
+}
+
 static hipError_t AllocZeroed(void **ptr, size_t bytes, int dev) {
   hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
   (void)hipThreadExchangeStreamCaptureMode(&mode);
-  static hipStream_t side[kMaxDevices] = {};
-  hipError_t e = hipSuccess;
-  if (dev < 0 || dev >= kMaxDevices) e = hipErrorInvalidDevice;
-  if (e == hipSuccess && side[dev] == nullptr)
-    e = hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking);
+  hipStream_t side = nullptr;
+  hipError_t e = SideStream(dev, &side);
   *ptr = nullptr;
   if (e == hipSuccess) e = hipMalloc(ptr, bytes);
-  if (e == hipSuccess) e = hipMemsetAsync(*ptr, 0, bytes, side[dev]);
-  if (e == hipSuccess) e = hipStreamSynchronize(side[dev]);
+  if (e == hipSuccess) e = hipMemsetAsync(*ptr, 0, bytes, side);
+  if (e == hipSuccess) e = hipStreamSynchronize(side);
   if (e != hipSuccess && *ptr != nullptr) {
     (void)hipFree(*ptr);
     *ptr = nullptr;
@@ -1094,6 +1104,23 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   const bool tall = UseTall(&pd, stream, /*dry=*/true);
   if (tall && UseTallPipe(p0, a.nonzeros / (kBlock * kBlock),
                           ((long long)a.cols + kBlock - 1) / kBlock, ta, tb)) {
+    // (the tall pipeline needs no workspace, but launches measurably slower
+    // -- config 5: 217 vs 198 us per launch, back to back on the null
+    // stream, r06 diag -- in a process where no non-blocking stream was
+    // created after the operands were allocated; until r06 the stray tile
+    // counter's allocation created the library's private stream here as a
+    // side effect. It is created explicitly now, once per device.)
+    {
+      std::lock_guard<std::mutex> lock(g_pairs_mu);
+      int dev = 0;
+      hipStream_t side = nullptr;
+      if (hipGetDevice(&dev) == hipSuccess) {
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        (void)SideStream(dev, &side);
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+      }
+    }
     GemmParams q = p0;
     q.persistent = 0;
     q.num_jtiles = q.j_limit / 512;
