@@ -330,6 +330,25 @@ __device__ __forceinline__ s16x8 read_mn(const char *img, int col0, int kk,
 
 // Maps the launch index to a tile index so that each XCD (blocks b and b+8
 // share one) walks a contiguous run of tiles. Bijective for any grid size.
+// The hardware deals workgroup b of a launch to XCD (b + r) mod 8, r a
+// rotation set by the device's dispatch history across queues (the same r
+// for every workgroup of one launch; it moves when another stream's work is
+// dispatched in between -- scripts/diag_xcc*.py). The XCD
+// tile maps below only need "b mod 8 = one XCD"; the speed skews (pair
+// placement, the tall pipeline's odd-XCD share) need the physical XCD,
+// read here from the XCC_ID hardware register.
+__device__ __forceinline__ int xcd_rotation() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return ((int)(v & 7u) - (int)(blockIdx.x & 7u)) & 7;
+}
+// 1 for logical XCD x (b mod 8) of this launch on a physically even XCD,
+// the faster half of the XCDs (~6% per block in the 4-wave
+// k-loop, ~20% in the tall pipeline). The placement knobs were tuned in
+// processes whose rotation was 7, where this equals x & 1 -- what they
+// used to read.
+__device__ __forceinline__ int fast_xcd(int x, int rot) { return ((x + rot) & 1) ^ 1; }
+
 __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
   const int xcd = bid & 7;
   const int q = nwg >> 3;
@@ -1606,12 +1625,15 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
       // (DSD only: measured there.)
       const bool xcd2 = !kOutT && p.pair_xcd2 != 0 && p.num_jtiles == 8 &&
                         n_solo == 0 && (half & 1) == 0;
+      // (modes 1 / 3 by physical XCD: which member of each logical XCD
+      // pair is fast depends on the launch's rotation, xcd_rotation)
+      const int rot = xcd2 ? xcd_rotation() : 0;
       auto place = [&](int b) {
         if (xcd2) {
           const int x = b & 7, k = b >> 3;
           panel = 2 * (x >> 1) + (k & 1);
           pi = p.pair_xcd2 == 2 ? 2 * (k >> 1) + (x & 1)
-             : ((x & 1) ^ (p.pair_xcd2 == 3 ? 1 : 0)) * (half >> 1) + (k >> 1);
+             : (fast_xcd(x, rot) ^ (p.pair_xcd2 == 3 ? 1 : 0)) * (half >> 1) + (k >> 1);
         } else {
           const int t = xcd_tile(b, n_light);
           panel = t / half;

@@ -1104,23 +1104,6 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   const bool tall = UseTall(&pd, stream, /*dry=*/true);
   if (tall && UseTallPipe(p0, a.nonzeros / (kBlock * kBlock),
                           ((long long)a.cols + kBlock - 1) / kBlock, ta, tb)) {
-    // (the tall pipeline needs no workspace, but launches measurably slower
-    // -- config 5: 217 vs 198 us per launch, back to back on the null
-    // stream, r06 diag -- in a process where no non-blocking stream was
-    // created after the operands were allocated; until r06 the stray tile
-    // counter's allocation created the library's private stream here as a
-    // side effect. It is created explicitly now, once per device.)
-    {
-      std::lock_guard<std::mutex> lock(g_pairs_mu);
-      int dev = 0;
-      hipStream_t side = nullptr;
-      if (hipGetDevice(&dev) == hipSuccess) {
-        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-        (void)hipThreadExchangeStreamCaptureMode(&mode);
-        (void)SideStream(dev, &side);
-        (void)hipThreadExchangeStreamCaptureMode(&mode);
-      }
-    }
     GemmParams q = p0;
     q.persistent = 0;
     q.num_jtiles = q.j_limit / 512;
