@@ -102,6 +102,7 @@ enum KnobId {
   kKnobTallOddShare,
   kKnobMinHandoff,
   kKnobXcdRows,
+  kKnobSddKrot,
   kNumKnobs
 };
 int Knob(KnobId k);

@@ -219,6 +219,10 @@ struct GemmParams {
   // XCD x takes a contiguous eighth of the rows over every panel
   // (dsd4w.hip; 0: the panel-major XCD map).
   int xcd_rows;
+  // 4-wave grouped SDD (not the K-split): start each group's k-walk at a
+  // rotated k-block (0 off; 1 by row, 2 by group index, 3 by tile, 4 by
+  // band of 8 rows; dsd4w.hip), a tuning experiment for power-of-two strides.
+  int sdd_krot;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

@@ -121,6 +121,7 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"tall_odd_share", "SPUTNIK_AMD_TALL_ODD_SHARE", 120, 50, 200},
     {"min_handoff", "SPUTNIK_AMD_MIN_HANDOFF", 2, 1, 64},
     {"xcd_rows", "SPUTNIK_AMD_XCD_ROWS", 1, 0, 1},
+    {"sdd_krot", "SPUTNIK_AMD_SDD_KROT", 0, 0, 4},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1171,6 +1172,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
   if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb, c.nonzeros / (kBlock * kBlock))) {
     p.sdd_order = Knob(kKnobSddOrder);
+    p.sdd_krot = Knob(kKnobSddKrot);
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
   }
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,

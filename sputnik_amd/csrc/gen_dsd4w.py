@@ -243,8 +243,10 @@ def switch():
 # Scalar load of the k-block (int16) of virtual entry min(s56, xlast) into
 # s59 (its half in s60), one block ahead of the SWITCH that uses it.
 def idx_load():
-    if VARIANT["sdd"]:  # k-block of virtual entry x is x
-        return ["s_min_u32 s59, s56, %[xlast]", "s_add_u32 s56, s56, 1", "s_mov_b32 s60, 0"]
+    if VARIANT["sdd"]:  # k-block of virtual entry x is its entry (x, or
+        # x rotated: dsd4w.hip sdd_krot)
+        return (["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"]
+                + entry_of("s78", "s59") + ["s_mov_b32 s60, 0"])
     out = ["s_min_u32 s78, s56, %[xlast]", "s_add_u32 s56, s56, 1"] + entry_of("s78", "s79")
     if col_order():
         out += ["s_lshl_b32 s74, s79, 2", "s_add_u32 s74, %[bolo], s74",
@@ -764,8 +766,9 @@ def prologue_setup():
     if col_order():
         out += ["s_lshr_b32 s77, %[bo0], 17", "s_lshl_b32 s76, %[bo0], 15",
                 "s_mov_b32 s63, %[bo1]"]
-    elif a_rows_t():  # entry 0: the panel's first k-block
-        out += ["s_mov_b32 s76, 0", "s_mov_b32 s77, 0"]
+    elif a_rows_t():  # entry 0's k-block of the panel
+        out += entry_of("s57", "s78") + ["s_mul_hi_u32 s77, s78, %[sk128]",
+                                         "s_mul_i32 s76, s78, %[sk128]"]
     else:
         hi, lo = s_block_shift()
         out += entry_of("s57", "s76")

@@ -418,6 +418,25 @@ def test_kat_sdd_grouped_pow2_stride(ta, tb, m, order):
     _equal(got, want, f"sdd pow2 {ta}{tb} m={m} order={order}")
 
 
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("krot", [1, 2, 3, 4])
+def test_kat_sdd_grouped_krot(ta, tb, krot):
+    """Grouped 4-wave SDD with the k-walk rotated (knob sdd_krot: each group
+    starts at its own k-block and wraps, through the kernel's two CSR
+    segments), K = 1152 (9 k-blocks, so every rotation wraps unevenly), banded
+    order over 32-KiB rows: exact on integer data."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    prev = sp.tuning("sdd_krot")
+    sp.tuning("sdd_krot", krot)
+    try:
+        got, want, plan = kat_sdd(2048, 1152, 16384, None, ta, tb, "f16", nb=4 * cus + 37,
+                                  seed=krot + 2 * ta + tb)
+    finally:
+        sp.tuning("sdd_krot", prev)
+    assert plan == 1, "grouped SDD tiles not selected"
+    _equal(got, want, f"sdd krot {krot} {ta}{tb}")
+
+
 # (m, k, n, stored blocks, dtype): one CU's workgroup per chunk, S picked
 # in-kernel from the group count (dsd4w.hip kKs): 8 rows x 60 blocks with
 # K = 2048 -> S = 8 (2 k-blocks per chunk, many partial groups); 150 blocks,
