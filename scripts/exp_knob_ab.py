@@ -43,14 +43,20 @@ def main():
             co = sp.Matrix(4096, 4096, pp.out)
             prob = types.SimpleNamespace(
                 launcher=lambda: (lambda: sp.MatmulEx(cg, False, pp.C, False, co)))
-    elif a.workload in ("moe_sdd", "moe_dsd", "moe"):  # config 4's products / step
+    elif a.workload in ("moe_sdd", "moe_dsd", "moe", "moe_sdd_nt"):  # config 4's products / step
         mp = bench.MoeProblem("bf16", 7, dev)
         t, dm, cols = mp.dims
         X, W1 = sp.Matrix(t, dm, mp.x), sp.Matrix(dm, cols, mp.w1)
+        if a.workload == "moe_sdd_nt":  # MegaBlocks' w1 layout [E d_ff][d_model]
+            w1t = mp.w1.view(dm, cols).t().contiguous()
+            W1T = sp.Matrix(cols, dm, w1t)
+            nt = lambda: sp.Matmul(X, False, W1T, True, mp.H)  # noqa: E731
         W2, Y = sp.Matrix(cols, dm, mp.w2), sp.Matrix(t, dm, mp.y)
         sdd = lambda: sp.Matmul(X, False, W1, False, mp.H)  # noqa: E731
         dsd = lambda: sp.MatmulEx(mp.H, False, W2, False, Y)  # noqa: E731
         f = {"moe_sdd": sdd, "moe_dsd": dsd}.get(a.workload, lambda: (sdd(), dsd()))
+        if a.workload == "moe_sdd_nt":
+            f = nt
         prob = types.SimpleNamespace(launcher=lambda: f)
     elif a.workload.startswith("op:"):  # op:OP:TRANS:DIM, e.g. op:sdd:NN:4096
         _, op, tr, dim = a.workload.split(":")

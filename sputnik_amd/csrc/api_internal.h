@@ -103,6 +103,7 @@ enum KnobId {
   kKnobMinHandoff,
   kKnobXcdRows,
   kKnobSddKrot,
+  kKnobSddSpread,
   kNumKnobs
 };
 int Knob(KnobId k);

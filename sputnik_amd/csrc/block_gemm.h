@@ -223,6 +223,12 @@ struct GemmParams {
   // rotated k-block (0 off; 1 by row, 2 by group index, 3 by tile, 4 by
   // band of 8 rows; dsd4w.hip), a tuning experiment for power-of-two strides.
   int sdd_krot;
+  // 4-wave grouped SDD, RB x GB block order over rows of equal count: the GB
+  // groups of a round taken G / GB apart along the row instead of adjacent
+  // (1; 0 adjacent), so its B columns span more of B's rows (dsd4w.hip;
+  // knob sdd_spread, on for NT by default). The blocks computed are the same
+  // either way: only which groups run side by side changes.
+  int sdd_spread;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one

@@ -122,6 +122,10 @@ static const KnobDef kKnobs[kNumKnobs] = {
     {"min_handoff", "SPUTNIK_AMD_MIN_HANDOFF", 2, 1, 64},
     {"xcd_rows", "SPUTNIK_AMD_XCD_ROWS", 1, 0, 1},
     {"sdd_krot", "SPUTNIK_AMD_SDD_KROT", 0, 0, 4},
+    // (2: NT only -- SDD NT 16384^3 dense 7603 -> 6934 us, config 4 in
+    // MegaBlocks' w1 layout 812 -> 805 us, other NT shapes a tie; NN / TT
+    // ties or noise, profiles/r06/ab/sdd_spread_ab.jsonl)
+    {"sdd_spread", "SPUTNIK_AMD_SDD_SPREAD", 2, 0, 2},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1173,6 +1177,8 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   if (Dsd4wEnabled() && Sdd4wApplies(p, grouped, ta, tb, c.nonzeros / (kBlock * kBlock))) {
     p.sdd_order = Knob(kKnobSddOrder);
     p.sdd_krot = Knob(kKnobSddKrot);
+    const int spread = Knob(kKnobSddSpread);
+    p.sdd_spread = spread == 1 || (spread == 2 && tb && !ta) ? 1 : 0;
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
   }
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,

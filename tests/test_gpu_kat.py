@@ -419,6 +419,36 @@ def test_kat_sdd_grouped_pow2_stride(ta, tb, m, order):
 
 
 @pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("spread", [0, 1, 2])
+def test_kat_sdd_uniform_rows_spread(ta, tb, spread):
+    """Grouped 4-wave SDD over rows of equal count (expert-block-diagonal:
+    4 experts x 8 rows x 64 blocks, 16 groups per row) in the 8 x 4 block
+    order, its 4 groups per round adjacent (sdd_spread 0) or 4 apart (1; 2,
+    the default: NT only): exact on integer data, block by block."""
+    rng = np.random.default_rng(11 + spread + 2 * ta + tb)
+    topo = mu.expert_block_diagonal(4, 8, 64)
+    m, k, n = 32 * 128, 256, 4 * 64 * 128
+    A = IDense(*((k, m) if ta else (m, k)), rng, "f16")
+    Bd = IDense(*((n, k) if tb else (k, n)), rng, "f16")
+    Cs = ISparse(m, n, None, rng, "f16", topology=topo)
+    Cs.dev.fill_(float("nan"))
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    prev = sp.tuning("sdd_spread", spread)
+    try:
+        kern = sp.sdd_kernel(A.m, ta, Bd.m, tb, Cs.m)
+        sp.Matmul(A.m, ta, Bd.m, tb, Cs.m)
+    finally:
+        sp.tuning("sdd_spread", prev)
+    assert kern == 3, "4-wave grouped SDD not selected"
+    a, b = _op(A.values, ta).astype(np.float64), _op(Bd.values, tb).astype(np.float64)
+    rows = np.repeat(np.arange(len(topo[0]) - 1), np.diff(topo[0]))
+    want = np.stack([a[r * B:(r + 1) * B] @ b[:, c * B:(c + 1) * B]
+                     for r, c in zip(rows, topo[1])])
+    _equal(Cs.dev, _expect(want, "f16"), f"sdd uniform spread={spread} {ta}{tb}")
+
+
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
 @pytest.mark.parametrize("krot", [1, 2, 3, 4])
 def test_kat_sdd_grouped_krot(ta, tb, krot):
     """Grouped 4-wave SDD with the k-walk rotated (knob sdd_krot: each group
