@@ -3,7 +3,9 @@
 kernel's LDS-DMA loads (buffer_load ... lds). Renders gen_dsd4w.py, appends
 the bits to every such load of the chosen macros, compiles dsd4w.hip against
 that body and links it with the tree's other objects (build/sputnik_amd).
-Usage: build_cp_variant.py NAME "BITS" [MACRO_SUBSTR]   -> build/exp/NAME.so"""
+Usage: build_cp_variant.py NAME "BITS" [MACRO_SUBSTR]   -> build/exp/NAME.so
+BITS = PLAINPUB instead: the pair / K-split partial publishes lose their sc1
+bit (the lines stay in the XCD's L2; same-XCD pairs only -- an experiment)."""
 import importlib.util
 import os
 import subprocess
@@ -23,7 +25,12 @@ def main():
     for line in gen.render().split("\n"):
         if line.startswith("#define "):
             cur = line.split()[1]
-        if ("buffer_load" in line and line.endswith(' lds\\n" \\') and only in cur):
+        if bits == "PLAINPUB":  # partial publishes without sc1 (kept in L2)
+            if ("buffer_store_dwordx4 a[" in line and " sc1\\n" in line and only in cur
+                    and "_KS" not in cur):  # (K-split chunks sit on other XCDs)
+                line = line.replace(" sc1\\n", "\\n")
+                n += 1
+        elif ("buffer_load" in line and line.endswith(' lds\\n" \\') and only in cur):
             line = line.replace(" lds\\n", " " + bits + " lds\\n")
             n += 1
         out.append(line)
