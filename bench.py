@@ -952,7 +952,10 @@ def main():
         per_step = ms / args.steps
         flops_all = sum_over_ranks(prob.flops, world)
         tflops = flops_all / (per_step * 1e-3) / 1e12
-        key = f"dsd_{m_total}x{args.k}x{args.n}_{d}_{args.dtype}"
+        # (keyed by this rank's own launch: at N > 1 a rank runs a panel of
+        # prob.m rows, which the N = 1 PMC pass of m_total rows does not
+        # describe, so its traffic stays null)
+        key = f"dsd_{prob.m}x{args.k}x{args.n}_{d}_{args.dtype}"
         traffic, note = pmc_traffic(args.pmc, key, build.get("hash"))
         roof = roofline(prob.flops, prob.bytes, per_step * 1e-3, prob.kernel,
                         traffic)
