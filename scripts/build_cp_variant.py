@@ -4,7 +4,8 @@ kernel's LDS-DMA loads (buffer_load ... lds). Renders gen_dsd4w.py, appends
 the bits to every such load of the chosen macros, compiles dsd4w.hip against
 that body and links it with the tree's other objects (build/sputnik_amd).
 Usage: build_cp_variant.py NAME "BITS" [MACRO_SUBSTR]   -> build/exp/NAME.so
-BITS = PLAINPUB instead: the pair / K-split partial publishes lose their sc1
+BITS = STORE:<bits> instead: the output stores' nt becomes <bits> (empty:
+plain). BITS = PLAINPUB: the pair / K-split partial publishes lose their sc1
 bit (the lines stay in the XCD's L2; same-XCD pairs only -- an experiment)."""
 import importlib.util
 import os
@@ -25,7 +26,11 @@ def main():
     for line in gen.render().split("\n"):
         if line.startswith("#define "):
             cur = line.split()[1]
-        if bits == "PLAINPUB":  # partial publishes without sc1 (kept in L2)
+        if bits.startswith("STORE:"):  # output stores: "offen nt" -> "offen <rest>"
+            if "buffer_store_dwordx4" in line and " offen nt\\n" in line and only in cur:
+                line = line.replace(" offen nt\\n", (" offen " + bits[6:]).rstrip() + "\\n")
+                n += 1
+        elif bits == "PLAINPUB":  # partial publishes without sc1 (kept in L2)
             if ("buffer_store_dwordx4 a[" in line and " sc1\\n" in line and only in cur
                     and "_KS" not in cur):  # (K-split chunks sit on other XCDs)
                 line = line.replace(" sc1\\n", "\\n")
