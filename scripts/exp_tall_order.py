@@ -54,9 +54,11 @@ def main():
                         ("dealt32", dealt[32]), ("dealt31", dealt[31])):
         o, i = permuted(off, idx, order)
         probs[name] = bench.DsdProblem(M, K, o, i, N, False, False, "f16", 0, dev)
+    if len(sys.argv) > 1:  # one variant only (for rocprofv3 --pmc passes)
+        probs = {sys.argv[1]: probs[sys.argv[1]]}
     fns = {k: p.launcher() for k, p in probs.items()}
     res = {k: [] for k in fns}
-    for _ in range(7):
+    for _ in range(7 if len(fns) > 1 else 1):
         for k, f in fns.items():
             for _ in range(20):
                 f()
