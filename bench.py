@@ -257,6 +257,7 @@ _SDD_KERNELS = {
     1: "block_gemm_kernel (SDD, 8-wave grouped 128x512 tiles)",
     2: "dsd4w_kernel (SDD NN, 4-wave grouped tiles, K split over workgroups)",
     3: "dsd4w_kernel (SDD, 4-wave grouped 128x512 tiles)",
+    4: "transpose16_kernel (B^T -> B) + dsd4w_kernel (SDD, 4-wave grouped 128x512 tiles)",
 }
 _DSD_KERNELS = {
     0: "block_gemm_kernel ({op}, 8-wave 128x512 tile)",

@@ -165,7 +165,10 @@ int sputnik_sdd_plan(const sputnik_matrix_t *a, int transpose_a,
                      const sputnik_block_matrix_t *c);
 /* The SDD kernel behind that plan: 0 = the 8-wave k-split block tile,
  * 1 = grouped tiles on the 8-wave kernel, 2 = the 4-wave K-split, 3 =
- * grouped tiles on the 4-wave kernel, -1 = rejected. */
+ * grouped tiles on the 4-wave kernel, 4 = (NT / TT over a B past the
+ * MALL) B transposed into a library buffer, then grouped tiles on the
+ * 4-wave kernel (eager launches; a stream being captured keeps 3), -1 =
+ * rejected. */
 int sputnik_sdd_kernel(const sputnik_matrix_t *a, int transpose_a,
                        const sputnik_matrix_t *b, int transpose_b,
                        const sputnik_block_matrix_t *c);

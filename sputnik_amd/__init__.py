@@ -368,8 +368,9 @@ def sdd_plan(a, transpose_a, b, transpose_b, c) -> int:
 
 def sdd_kernel(a, transpose_a, b, transpose_b, c) -> int:
     """The kernel behind sdd_plan's tile plan: 0 8-wave k-split block tile,
-    1 8-wave grouped, 2 4-wave K-split, 3 4-wave grouped, -1 rejected
-    (sputnik_sdd_kernel)."""
+    1 8-wave grouped, 2 4-wave K-split, 3 4-wave grouped, 4 B transposed
+    into a library buffer then 4-wave grouped (NT / TT over a large B), -1
+    rejected (sputnik_sdd_kernel)."""
     ca, cb, cc = a._c(), b._c(), c._c()
     return int(lib().sputnik_sdd_kernel(ctypes.byref(ca), int(bool(transpose_a)),
                                         ctypes.byref(cb), int(bool(transpose_b)),

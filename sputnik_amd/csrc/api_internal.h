@@ -104,6 +104,7 @@ enum KnobId {
   kKnobXcdRows,
   kKnobSddKrot,
   kKnobSddSpread,
+  kKnobSddBtMinMib,
   kNumKnobs
 };
 int Knob(KnobId k);

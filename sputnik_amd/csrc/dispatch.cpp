@@ -26,6 +26,7 @@
 #include "api_internal.h"
 #include "block_gemm.h"
 #include "dsd4w.h"
+#include "layout.h"
 #include "metadata.h"
 #include "sputnik/sputnik.h"
 #include "sputnik_amd.h"
@@ -126,6 +127,9 @@ static const KnobDef kKnobs[kNumKnobs] = {
     // MegaBlocks' w1 layout 812 -> 805 us, other NT shapes a tie; NN / TT
     // ties or noise, profiles/r06/ab/sdd_spread_ab.jsonl)
     {"sdd_spread", "SPUTNIK_AMD_SDD_SPREAD", 2, 0, 2},
+    // (SDD NT / TT: B transposed first when its K N 2 bytes reach this many
+    // MiB -- the MALL's 256 MB -- and the product is dense enough; 0 off)
+    {"sdd_bt_min_mib", "SPUTNIK_AMD_SDD_BT_MIN_MIB", 256, 0, 1 << 20},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1163,6 +1167,83 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
                          /*out_t=*/true, tall, p, stream);
 }
 
+// ---- SDD with B stored transposed, over operands past the MALL -------------
+// SDD NT / TT read B^T's rows 256 B per k-block. While A and B fit the
+// 256-MB Infinity Cache (MALL) that costs nothing (NT 8192^3 runs at NN's
+// speed), past it the misses go to HBM: SDD NT 16384^3 at 50% ran 5231 us
+// against NN's 3516. There, B is transposed
+// once into a library-owned buffer ([K][N], layout.hip, ~2 K N 2 bytes of
+// HBM traffic) and the N-major kernel (NN / TN) runs on it. Gate: B's
+// K N 2 bytes >= knob sdd_bt_min_mib MiB, and the product's FLOPs per byte
+// of B (blocks 128^2 2 K / (K N 2) = 16384 blocks / N) >= kBtMinRatio, so
+// the copy is a small part of the launch (16384^3: 50% 8192, dense 16384,
+// 10% 1639 -- below; MegaBlocks' x.w1^T 1024 -- below); the N-major path
+// must be the 4-wave grouped kernel. Eager launches only: a stream being
+// captured keeps the NT / TT kernel (the buffer is allocated on first use).
+// One buffer per (device, stream), grown as needed, kept for the process
+// (INTEGRATION.md 3b); stream order makes it safe to reuse.
+constexpr long long kBtMinRatio = 3000;
+struct BtSlot {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  void *data = nullptr;
+  size_t bytes = 0;
+};
+static BtSlot g_bt[kMaxPairSlots];
+
+static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
+                           const BlockMatrix &c, hipStream_t stream) {
+  if (!tb || stream == hipStreamPerThread) return false;  // (many streams, one handle)
+  const long long min_mib = Knob(kKnobSddBtMinMib);
+  if (min_mib <= 0) return false;
+  const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
+  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
+  const long long blocks = c.nonzeros / (kBlock * kBlock);
+  if (blocks * 16384 < kBtMinRatio * n) return false;
+  unsigned long long id = 0;
+  if (CaptureState(stream, &id) != 0) return false;
+  GemmParams p;
+  const Matrix bt((int)k, (int)n, b.data);
+  return PrepareSdd(a, ta, bt, false, c, &p) == Status::kOk && UseGroupedSdd(&p, c, false) &&
+         Dsd4wEnabled() && Sdd4wApplies(p, true, ta, false, blocks);
+}
+
+// The transposed-B buffer of (device, stream), at least `bytes` (nullptr:
+// none -- the table is full or the allocation failed; the caller keeps the
+// NT / TT kernel).
+static void *BtBuffer(hipStream_t stream, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(g_pairs_mu);
+  BtSlot *slot = nullptr;
+  for (BtSlot &s : g_bt)
+    if (s.data != nullptr && s.device == dev && s.stream == stream) slot = &s;
+  if (slot == nullptr)
+    for (BtSlot &s : g_bt)
+      if (s.data == nullptr) {
+        slot = &s;
+        break;
+      }
+  if (slot == nullptr) return nullptr;
+  if (slot->bytes < bytes) {
+    if (slot->data != nullptr) {
+      // the stream's earlier launches may still read the old buffer
+      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+      FreeQuiet(slot->data);
+      slot->data = nullptr;
+      slot->bytes = 0;
+    }
+    if (hipMalloc(&slot->data, bytes) != hipSuccess) {
+      slot->data = nullptr;
+      return nullptr;
+    }
+    slot->bytes = bytes;
+    slot->device = dev;
+    slot->stream = stream;
+  }
+  return slot->data;
+}
+
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
                   const BlockMatrix &c, int dtype, hipStream_t stream,
                   Status *st_out) {
@@ -1170,6 +1251,14 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   const Status st = PrepareSdd(a, ta, b, tb, c, &p);
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
+  if (UseBtTranspose(a, ta, b, tb, c, stream)) {
+    void *bt = BtBuffer(stream, (size_t)b.rows * b.cols * 2);
+    if (bt != nullptr) {
+      const hipError_t e = LaunchTranspose16(b.data, b.rows, b.cols, bt, stream);
+      if (e != hipSuccess) return e;
+      return RunSdd(a, ta, Matrix(b.cols, b.rows, bt), false, c, dtype, stream, st_out);
+    }
+  }
   p.debug = g_debug;
   const bool grouped = UseGroupedSdd(&p, c, tb);
   if (!grouped && PrepareSddKsplit(&p, c, ta, tb, stream))
@@ -1465,6 +1554,9 @@ int SddKernel(const void *a, bool ta, const void *b, bool tb, const void *c) {
   if (plan != 1) return plan;
   GemmParams p;
   const BlockMatrix &cm = *static_cast<const BlockMatrix *>(c);
+  if (UseBtTranspose(*static_cast<const Matrix *>(a), ta, *static_cast<const Matrix *>(b),
+                     tb, cm, nullptr))
+    return 4;
   if (PrepareSdd(*static_cast<const Matrix *>(a), ta,
                  *static_cast<const Matrix *>(b), tb, cm, &p) != Status::kOk ||
       !UseGroupedSdd(&p, cm, tb))

@@ -418,6 +418,70 @@ def test_kat_sdd_grouped_pow2_stride(ta, tb, m, order):
     _equal(got, want, f"sdd pow2 {ta}{tb} m={m} order={order}")
 
 
+@pytest.fixture
+def bt_small():
+    """The transposed-B SDD path (dispatch.cpp UseBtTranspose) from a 1-MiB
+    B on (default: 256 MiB, the MALL), so small problems take it."""
+    prev = sp.tuning("sdd_bt_min_mib", 1)
+    yield
+    sp.tuning("sdd_bt_min_mib", prev)
+
+
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("dtype,k", [("f16", 512), ("bf16", 256)])
+def test_kat_sdd_bt_transpose(ta, dtype, k, bt_small):
+    """SDD NT / TT with B^T transposed into the library's buffer first
+    (sputnik_sdd_kernel 4), then the grouped 4-wave NN / TN kernel: exact,
+    and the same again with the buffer reused and then grown (N 4096 ->
+    6144), and with the path off (knob 0: the NT / TT kernel, 3). (M =
+    8192: A^T's rows 16 KiB apart, so TN stays on the 4-wave kernel.)"""
+    for n, seed in ((4096, 1), (4096, 2), (6144, 3)):
+        rng = np.random.default_rng(seed + 10 * ta)
+        m = 8192
+        A = IDense(*((k, m) if ta else (m, k)), rng, dtype)
+        Bd = IDense(n, k, rng, dtype)  # B^T stored [N][K]
+        Cs = ISparse(m, n, 0.6, rng, dtype)
+        Cs.dev.fill_(float("nan"))
+        sp.AllocateRowIndicesBuffer(Cs.m)
+        sp.RowIndices(Cs.m, Cs.m.row_indices)
+        assert sp.sdd_kernel(A.m, ta, Bd.m, True, Cs.m) == 4
+        sp.Matmul(A.m, ta, Bd.m, True, Cs.m)
+        full = _op(A.values, ta).astype(np.float64) @ Bd.values.T
+        want = _expect(Cs.blocks_of(full), dtype)
+        _equal(Cs.dev, want, f"sdd bt {'T' if ta else 'N'}T {dtype} n={n}")
+    prev = sp.tuning("sdd_bt_min_mib", 0)
+    try:
+        assert sp.sdd_kernel(A.m, ta, Bd.m, True, Cs.m) == 3
+        Cs.dev.fill_(float("nan"))
+        sp.Matmul(A.m, ta, Bd.m, True, Cs.m)
+        _equal(Cs.dev, want, "sdd bt path off")
+    finally:
+        sp.tuning("sdd_bt_min_mib", prev)
+
+
+def test_graph_capture_sdd_bt_keeps_nt_kernel(bt_small):
+    """A captured SDD NT that would take the transposed-B path eagerly runs
+    the NT kernel inside the capture (no buffer is allocated or used by a
+    graph); replays are exact."""
+    rng = np.random.default_rng(21)
+    m, k, n = 16384, 256, 2048
+    A = IDense(m, k, rng, "f16")
+    Bd = IDense(n, k, rng, "f16")
+    Cs = ISparse(m, n, 0.6, rng, "f16")
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    want = _expect(Cs.blocks_of(A.values.astype(np.float64) @ Bd.values.T), "f16")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        sp.Matmul(A.m, False, Bd.m, True, Cs.m)
+    for _ in range(2):
+        Cs.dev.fill_(float("nan"))
+        g.replay()
+        _equal(Cs.dev, want, "captured sdd nt")
+
+
 @pytest.mark.parametrize("ta,tb", TRANSPOSES)
 @pytest.mark.parametrize("spread", [0, 1, 2])
 def test_kat_sdd_uniform_rows_spread(ta, tb, spread):
