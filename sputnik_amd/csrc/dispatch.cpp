@@ -1190,6 +1190,10 @@ struct BtSlot {
   size_t bytes = 0;
 };
 static BtSlot g_bt[kMaxPairSlots];
+// Held from choosing the buffer until the transpose and the product are
+// enqueued, so another thread cannot grow (free) the buffer of the same
+// stream in between; taken before g_pairs_mu, never while holding it.
+static std::mutex g_bt_mu;
 
 static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
                            const BlockMatrix &c, hipStream_t stream) {
@@ -1210,11 +1214,10 @@ static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
 
 // The transposed-B buffer of (device, stream), at least `bytes` (nullptr:
 // none -- the table is full or the allocation failed; the caller keeps the
-// NT / TT kernel).
+// NT / TT kernel). Caller holds g_bt_mu.
 static void *BtBuffer(hipStream_t stream, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(g_pairs_mu);
   BtSlot *slot = nullptr;
   for (BtSlot &s : g_bt)
     if (s.data != nullptr && s.device == dev && s.stream == stream) slot = &s;
@@ -1252,6 +1255,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
   if (UseBtTranspose(a, ta, b, tb, c, stream)) {
+    std::lock_guard<std::mutex> lock(g_bt_mu);
     void *bt = BtBuffer(stream, (size_t)b.rows * b.cols * 2);
     if (bt != nullptr) {
       const hipError_t e = LaunchTranspose16(b.data, b.rows, b.cols, bt, stream);

@@ -459,6 +459,43 @@ def test_kat_sdd_bt_transpose(ta, dtype, k, bt_small):
         sp.tuning("sdd_bt_min_mib", prev)
 
 
+def test_sdd_bt_two_threads_one_stream(bt_small):
+    """Two host threads issue SDD NT on one stream, one of them with a larger
+    B (so the stream's transposed-B buffer grows while the other thread's
+    launches may be queued): every result exact (dispatch.cpp g_bt_mu)."""
+    import threading
+    probs = []
+    for n, seed in ((4096, 31), (6144, 32)):
+        rng = np.random.default_rng(seed)
+        A = IDense(8192, 256, rng, "f16")
+        Bd = IDense(n, 256, rng, "f16")
+        Cs = ISparse(8192, n, 0.6, rng, "f16")
+        sp.AllocateRowIndicesBuffer(Cs.m)
+        sp.RowIndices(Cs.m, Cs.m.row_indices)
+        want = _expect(Cs.blocks_of(A.values.astype(np.float64) @ Bd.values.T), "f16")
+        probs.append((A, Bd, Cs, want))
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    errors = []
+
+    def work(A, Bd, Cs):
+        try:
+            for _ in range(4):
+                sp.Matmul(A.m, False, Bd.m, True, Cs.m, stream=s.cuda_stream)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=pr[:3]) for pr in probs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    s.synchronize()
+    assert not errors, errors
+    for A, Bd, Cs, want in probs:
+        _equal(Cs.dev, want, f"sdd bt threads n={Bd.m.rows}")
+
+
 def test_graph_capture_sdd_bt_keeps_nt_kernel(bt_small):
     """A captured SDD NT that would take the transposed-B path eagerly runs
     the NT kernel inside the capture (no buffer is allocated or used by a
