@@ -105,6 +105,7 @@ enum KnobId {
   kKnobSddKrot,
   kKnobSddSpread,
   kKnobSddBtMinMib,
+  kKnobSddTailMinK,
   kNumKnobs
 };
 int Knob(KnobId k);

@@ -229,6 +229,12 @@ struct GemmParams {
   // knob sdd_spread, on for NT by default). The blocks computed are the same
   // either way: only which groups run side by side changes.
   int sdd_spread;
+  // SDD tail split (knob sdd_tail; sdd_tail_rows below): the grouped 4-wave
+  // launch takes C's rows [0, R0) and an 8-wave launch of one block per
+  // workgroup the stored blocks of rows [R0, R), so the groups' last round
+  // is not a few groups on an idle chip. tail_cus: the CUs (the round size).
+  int sdd_tail;
+  int tail_cus;
 };
 
 // XOR key of the m/n-contiguous image: spreads the 8 k-rows one
@@ -358,6 +364,85 @@ __device__ __forceinline__ int xcd_rotation() {
 // processes whose rotation was 7, where this equals x & 1 -- what they
 // used to read.
 __device__ __forceinline__ int fast_xcd(int x, int rot) { return ((x + rot) & 1) ^ 1; }
+
+// SDD tail split (GemmParams::sdd_tail). The grouped SDD runs one group of
+// up to 4 stored blocks of a row per workgroup, G = sum_r ceil(n_r / 4)
+// groups in rounds of `cus`: with G = 2 cus + 24 (SDD 8192^3 at 50%: 536
+// groups) the third round is 24 groups, as long as a full round, on an idle
+// chip. When that last round holds at most cus / 4 groups, R0 = the most
+// rows [0, R0) whose groups fit the full rounds (G(R0) <= G - G % cus);
+// the stored blocks of rows [R0, R) -- at most cus of them, else no split --
+// go to one 8-wave launch of a block per workgroup (~2/3 of a grouped round
+// at K = 8192: 8192^3 50% 511 -> 454 us).
+// Rows of equal count (group-major orders) are not split. Every workgroup of
+// both launches computes the same R0 from C's offsets (deterministic); R0 ==
+// R: no split. scratch: >= 2 kThreads / 64 + 2 ints of LDS, free.
+template <int kThreads>
+__device__ int sdd_tail_rows(const GemmParams &p, int *scratch, int tid) {
+  constexpr int kWaves = kThreads / 64;
+  const int R = p.num_rows, cus = p.tail_cus;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    scratch[kWaves] = 0x7fffffff;  // fewest groups in a row
+    scratch[kWaves + 1] = 0;       // most groups in a row
+  }
+  __syncthreads();
+  const int per = (R + kThreads - 1) / kThreads;
+  const int r0 = min(R, tid * per), r1 = min(R, r0 + per);
+  int local = 0, gmin = 0x7fffffff, gmax = 0;
+  for (int r = r0; r < r1; ++r) {
+    const int g = (p.c_offsets[r + 1] - p.c_offsets[r] + 3) / 4;
+    local += g;
+    gmin = min(gmin, g);
+    gmax = max(gmax, g);
+  }
+  int incl = local;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    gmin = min(gmin, __shfl_xor(gmin, d, 64));
+    gmax = max(gmax, __shfl_xor(gmax, d, 64));
+  }
+  if (lane == 63) scratch[wave] = incl;
+  if (lane == 0) {
+    atomicMin(&scratch[kWaves], gmin);
+    atomicMax(&scratch[kWaves + 1], gmax);
+  }
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int w = 0; w < kWaves; ++w) {
+    before += w < wave ? scratch[w] : 0;
+    total += scratch[w];
+  }
+  const bool uniform = scratch[kWaves] == scratch[kWaves + 1];
+  __syncthreads();
+  // (a last round of at most a quarter of the CUs: one block per workgroup
+  // on the 8-wave tile takes ~2/3 of a grouped round at K = 8192, so a
+  // fuller round is better left alone -- SDD 8192^3 at 30%, 84 groups past
+  // two rounds: 332 -> 340 us split)
+  const int rem = cus > 0 ? total % cus : 0;
+  if (uniform || rem == 0 || rem > cus / 4 || total <= rem) return R;  // (block-uniform)
+  // the most rows whose groups fit the full rounds: G(r) <= cap
+  const int cap = total - rem;
+  int cum = before + incl - local, best = -1;
+  if (r0 < R && cum <= cap) best = r0;
+  for (int r = r0; r < r1; ++r) {
+    cum += (p.c_offsets[r + 1] - p.c_offsets[r] + 3) / 4;
+    if (cum <= cap) best = r + 1;
+  }
+  if (tid == 0) scratch[0] = 0;
+  __syncthreads();
+  if (best > 0) atomicMax(&scratch[0], best);
+  __syncthreads();
+  const int cand = scratch[0];
+  __syncthreads();  // scratch reads done
+  const int tail = p.c_offsets[R] - p.c_offsets[cand];
+  return tail > 0 && tail <= cus ? cand : R;
+}
 
 __device__ __forceinline__ int xcd_tile(int bid, int nwg) {
   const int xcd = bid & 7;
@@ -1852,10 +1937,18 @@ __global__ void __launch_bounds__(64 * Cfg::kWaves,
         entry0 = p.s_offsets[srow];
         entries = p.s_offsets[srow + 1] - entry0;
       } else if constexpr (kSparseOut) {
-        out_block = tile;
-        grp_b0 = tile;
-        srow = p.c_row_indices[tile];
-        j0 = p.c_indices[tile] * kBlock;
+        int t = tile;
+        if (p.sdd_tail != 0) {
+          // tail launch (GemmParams::sdd_tail): workgroup b takes stored
+          // block offsets[R0] + b of the rows the grouped launch left
+          const int r_tail = sdd_tail_rows<kThreads>(p, reinterpret_cast<int *>(lds), tid);
+          t = p.c_offsets[r_tail] + (int)blockIdx.x;
+          if (r_tail == p.num_rows || t >= p.c_offsets[p.num_rows]) return;
+        }
+        out_block = t;
+        grp_b0 = t;
+        srow = p.c_row_indices[t];
+        j0 = p.c_indices[t] * kBlock;
       } else {
         // Longest-processing-time order: within each dense panel, tile t takes
         // the block-row with the t-th most nonzeros (ties by row index), so

@@ -130,6 +130,9 @@ static const KnobDef kKnobs[kNumKnobs] = {
     // (SDD NT / TT: B transposed first when its K N 2 bytes reach this many
     // MiB -- the MALL's 256 MB -- and the product is dense enough; 0 off)
     {"sdd_bt_min_mib", "SPUTNIK_AMD_SDD_BT_MIN_MIB", 256, 0, 1 << 20},
+    // (grouped 4-wave SDD with K >= this: the rows past the groups' full
+    // rounds go to an 8-wave launch of a block per workgroup; 0 off)
+    {"sdd_tail_min_k", "SPUTNIK_AMD_SDD_TAIL_MIN_K", 8192, 0, 1 << 30},
 };
 constexpr int kKnobUnset = -0x7fffffff - 1;
 static std::atomic<int> g_knobs[kNumKnobs];
@@ -1264,6 +1267,7 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
     }
   }
   p.debug = g_debug;
+  const int blocks = p.num_tiles;
   const bool grouped = UseGroupedSdd(&p, c, tb);
   if (!grouped && PrepareSddKsplit(&p, c, ta, tb, stream))
     return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
@@ -1272,7 +1276,31 @@ hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
     p.sdd_krot = Knob(kKnobSddKrot);
     const int spread = Knob(kKnobSddSpread);
     p.sdd_spread = spread == 1 || (spread == 2 && tb && !ta) ? 1 : 0;
-    return LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
+    // Tail split (block_gemm.h sdd_tail_rows): with K >= sdd_tail_min_k a
+    // grouped round is long, so the rows past the full rounds are better
+    // served one block per workgroup by the 8-wave k-split tile, launched
+    // right behind on the same stream (both launches find the same R0).
+    // Only while A and B fit the 256-MB MALL: that tile streams a whole
+    // row panel of A and column panel of B per block, and past the MALL it
+    // ran slower than the round it saves (SDD 16384^3 50%: NN 3428 -> 3644
+    // us, 8192^3 50%: 494 -> 445 us, profiles/r06/ab/sdd_tail_ab.jsonl).
+    int dev = 0;
+    const long long tail_k = Knob(kKnobSddTailMinK);
+    const long long ab_bytes = 2LL * p.k_limit * ((long long)p.num_rows * kBM + p.j_limit);
+    const bool tail = tail_k > 0 && p.k_limit >= tail_k && ab_bytes <= (256LL << 20) &&
+                      hipGetDevice(&dev) == hipSuccess && DeviceCUs(dev) > 0;
+    if (tail) {
+      p.sdd_tail = 1;
+      p.tail_cus = DeviceCUs(dev);
+    }
+    const hipError_t e = LaunchSdd4w(dtype, p, ta, tb, Dsd4wEpi(), stream);
+    if (e != hipSuccess || !tail) return e;
+    GemmParams q = p;
+    q.num_tiles = blocks;
+    q.grid = p.tail_cus;
+    q.sdd_order = 0;
+    return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
+                           /*grouped=*/false, q, stream);
   }
   return LaunchBlockGemm(dtype, true, /*s_kc=*/!ta, /*d_kc=*/tb, false,
                          grouped, p, stream);

@@ -171,7 +171,7 @@ def test_tuning_knobs_host_only():
                 "sdd4w_max_ld": 16384, "pair_fault": 0, "sdd_ksplit": 1,
                 "sdd_ksplit_min_k": 6144, "sdd_order": 1, "tall4w": 1,
                 "tall_flush_w": 4, "tall_odd_share": 120,
-                "min_handoff": 2, "xcd_rows": 1, "sdd_krot": 0, "sdd_spread": 2, "sdd_bt_min_mib": 256}
+                "min_handoff": 2, "xcd_rows": 1, "sdd_krot": 0, "sdd_spread": 2, "sdd_bt_min_mib": 256, "sdd_tail_min_k": 8192}
     for name, v in defaults.items():
         if "SPUTNIK_AMD_" + name.upper() not in _os.environ:
             assert sp.tuning(name) == v, name

@@ -459,6 +459,45 @@ def test_kat_sdd_bt_transpose(ta, dtype, k, bt_small):
         sp.tuning("sdd_bt_min_mib", prev)
 
 
+@pytest.mark.parametrize("ta,tb", TRANSPOSES)
+@pytest.mark.parametrize("case", ["tail", "uniform"])
+def test_kat_sdd_tail_split(ta, tb, case):
+    """SDD tail split (block_gemm.h sdd_tail_rows, knob sdd_tail_min_k
+    lowered so K = 256 takes it): 8192^2 at 50% has 2 x 256 + a few groups
+    of 4 blocks, so the grouped 4-wave launch takes the rows of the full
+    rounds and an 8-wave launch of a block per workgroup the rest; rows of
+    equal count are never split (the 8-wave launch then exits). Every
+    stored block exact, against the split off."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(41 + 2 * ta + tb)
+    m = n = 8192
+    k = 256
+    topo = mu.expert_block_diagonal(4, 16, 16) if case == "uniform" else None
+    A = IDense(*((k, m) if ta else (m, k)), rng, "f16")
+    Bd = IDense(*((n, k) if tb else (k, n)), rng, "f16")
+    Cs = ISparse(m, n, 0.5, rng, "f16", topology=topo)
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    if case == "tail":
+        groups = int(((np.diff(Cs.offsets) + 3) // 4).sum())
+        assert 0 < groups % cus <= cus // 4, groups  # a short last round
+    want = _expect(Cs.blocks_of(_op(A.values, ta).astype(np.float64) @ _op(Bd.values, tb)),
+                   "f16")
+    prev = sp.tuning("sdd_tail_min_k", 256)
+    try:
+        assert sp.sdd_kernel(A.m, ta, Bd.m, tb, Cs.m) == 3
+        for _ in range(2):
+            Cs.dev.fill_(float("nan"))
+            sp.Matmul(A.m, ta, Bd.m, tb, Cs.m)
+            _equal(Cs.dev, want, f"sdd tail {case} {ta}{tb}")
+        sp.tuning("sdd_tail_min_k", 0)
+        Cs.dev.fill_(float("nan"))
+        sp.Matmul(A.m, ta, Bd.m, tb, Cs.m)
+        _equal(Cs.dev, want, f"sdd tail off {case} {ta}{tb}")
+    finally:
+        sp.tuning("sdd_tail_min_k", prev)
+
+
 def test_sdd_bt_two_threads_one_stream(bt_small):
     """Two host threads issue SDD NT on one stream, one of them with a larger
     B (so the stream's transposed-B buffer grows while the other thread's
