@@ -1094,6 +1094,105 @@ static bool UseTallPipe(const GemmParams &p, long long blocks, long long row_max
          p.j_limit / 512 < 256;
 }
 
+// ---- SDD with B stored transposed, over operands past the MALL -------------
+// SDD NT / TT read B^T's rows 256 B per k-block. While A and B fit the
+// 256-MB Infinity Cache (MALL) that costs nothing (NT 8192^3 runs at NN's
+// speed), past it the misses go to HBM: SDD NT 16384^3 at 50% ran 5231 us
+// against NN's 3516 (DESIGN.md section 9 item 4). There, B is transposed
+// once into a library-owned buffer ([K][N], layout.hip, ~2 K N 2 bytes of
+// HBM traffic) and the N-major kernel (NN / TN) runs on it. Gate: B's
+// K N 2 bytes >= knob sdd_bt_min_mib MiB, and the product's FLOPs per byte
+// of B (blocks 128^2 2 K / (K N 2) = 16384 blocks / N) >= kBtMinRatio, so
+// the copy is a small part of the launch (16384^3: 50% 8192, dense 16384,
+// 10% 1639 -- below; MegaBlocks' x.w1^T 1024 -- below); the N-major path
+// must be the 4-wave grouped kernel. Eager launches only: a stream being
+// captured keeps the NT / TT kernel (the buffer is allocated on first use).
+// One buffer per (device, stream), grown as needed, kept for the process
+// (INTEGRATION.md 3b); stream order makes it safe to reuse.
+constexpr long long kBtMinRatio = 3000;
+struct BtSlot {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  void *data = nullptr;
+  size_t bytes = 0;
+};
+static BtSlot g_bt[kMaxPairSlots];
+// Held from choosing the buffer until the transpose and the product are
+// enqueued, so another thread cannot grow (free) the buffer of the same
+// stream in between; taken before g_pairs_mu, never while holding it.
+static std::mutex g_bt_mu;
+
+static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
+                           const BlockMatrix &c, hipStream_t stream) {
+  if (!tb || stream == hipStreamPerThread) return false;  // (many streams, one handle)
+  const long long min_mib = Knob(kKnobSddBtMinMib);
+  if (min_mib <= 0) return false;
+  const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
+  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
+  const long long blocks = c.nonzeros / (kBlock * kBlock);
+  if (blocks * 16384 < kBtMinRatio * n) return false;
+  unsigned long long id = 0;
+  if (CaptureState(stream, &id) != 0) return false;
+  GemmParams p;
+  const Matrix bt((int)k, (int)n, b.data);
+  return PrepareSdd(a, ta, bt, false, c, &p) == Status::kOk && UseGroupedSdd(&p, c, false) &&
+         Dsd4wEnabled() && Sdd4wApplies(p, true, ta, false, blocks);
+}
+
+// The same for DSD NT over a nearly dense A (out = A . B with B^T stored
+// [N][K] past the MALL): the sweep's DSD NT 16384^3 dense ran 7620 us
+// against NN's 6354, while at 50% NT is as fast as NN (3352 vs 3397 us), so
+// the gate asks for >= kDsdBtMinRatio FLOPs per byte of B, 16384 blocks / K
+// (16384^3: dense 16384, 50% 8192).
+constexpr long long kDsdBtMinRatio = 15000;
+static bool UseBtTransposeDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
+                              hipStream_t stream) {
+  if (!tb || ta || stream == hipStreamPerThread) return false;
+  const long long min_mib = Knob(kKnobSddBtMinMib);
+  if (min_mib <= 0) return false;
+  const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
+  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
+  const long long blocks = a.nonzeros / (kBlock * kBlock);
+  if (blocks * 16384 < kDsdBtMinRatio * k) return false;
+  unsigned long long id = 0;
+  return CaptureState(stream, &id) == 0;
+}
+
+// The transposed-B buffer of (device, stream), at least `bytes` (nullptr:
+// none -- the table is full or the allocation failed; the caller keeps the
+// NT / TT kernel). Caller holds g_bt_mu.
+static void *BtBuffer(hipStream_t stream, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  BtSlot *slot = nullptr;
+  for (BtSlot &s : g_bt)
+    if (s.data != nullptr && s.device == dev && s.stream == stream) slot = &s;
+  if (slot == nullptr)
+    for (BtSlot &s : g_bt)
+      if (s.data == nullptr) {
+        slot = &s;
+        break;
+      }
+  if (slot == nullptr) return nullptr;
+  if (slot->bytes < bytes) {
+    if (slot->data != nullptr) {
+      // the stream's earlier launches may still read the old buffer
+      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+      FreeQuiet(slot->data);
+      slot->data = nullptr;
+      slot->bytes = 0;
+    }
+    if (hipMalloc(&slot->data, bytes) != hipSuccess) {
+      slot->data = nullptr;
+      return nullptr;
+    }
+    slot->bytes = bytes;
+    slot->device = dev;
+    slot->stream = stream;
+  }
+  return slot->data;
+}
+
 hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
                   const Matrix &c, int dtype, bool build_meta,
                   hipStream_t stream, Status *st_out) {
@@ -1102,6 +1201,16 @@ hipError_t RunDsd(const BlockMatrix &a, bool ta, const Matrix &b, bool tb,
   const Status st = PrepareDsd(a, ta, b, tb, c, &p, &needs_meta);
   *st_out = st;
   if (st != Status::kOk) return hipSuccess;
+  if (UseBtTransposeDsd(a, ta, b, tb, stream)) {
+    std::lock_guard<std::mutex> lock(g_bt_mu);
+    void *bt = BtBuffer(stream, (size_t)b.rows * b.cols * 2);
+    if (bt != nullptr) {
+      const hipError_t e = LaunchTranspose16(b.data, b.rows, b.cols, bt, stream);
+      if (e != hipSuccess) return e;
+      return RunDsd(a, ta, Matrix(b.cols, b.rows, bt), false, c, dtype, build_meta, stream,
+                    st_out);
+    }
+  }
   if (needs_meta && build_meta) {
     const hipError_t e = BuildTransposed(a, stream);
     if (e != hipSuccess) return e;
@@ -1168,86 +1277,6 @@ hipError_t RunDds(const Matrix &a, bool ta, const BlockMatrix &b, bool tb,
   }
   return LaunchBlockGemm(dtype, false, /*s_kc=*/tb, /*d_kc=*/!ta,
                          /*out_t=*/true, tall, p, stream);
-}
-
-// ---- SDD with B stored transposed, over operands past the MALL -------------
-// SDD NT / TT read B^T's rows 256 B per k-block. While A and B fit the
-// 256-MB Infinity Cache (MALL) that costs nothing (NT 8192^3 runs at NN's
-// speed), past it the misses go to HBM: SDD NT 16384^3 at 50% ran 5231 us
-// against NN's 3516 (DESIGN.md section 9 item 4). There, B is transposed
-// once into a library-owned buffer ([K][N], layout.hip, ~2 K N 2 bytes of
-// HBM traffic) and the N-major kernel (NN / TN) runs on it. Gate: B's
-// K N 2 bytes >= knob sdd_bt_min_mib MiB, and the product's FLOPs per byte
-// of B (blocks 128^2 2 K / (K N 2) = 16384 blocks / N) >= kBtMinRatio, so
-// the copy is a small part of the launch (16384^3: 50% 8192, dense 16384,
-// 10% 1639 -- below; MegaBlocks' x.w1^T 1024 -- below); the N-major path
-// must be the 4-wave grouped kernel. Eager launches only: a stream being
-// captured keeps the NT / TT kernel (the buffer is allocated on first use).
-// One buffer per (device, stream), grown as needed, kept for the process
-// (INTEGRATION.md 3b); stream order makes it safe to reuse.
-constexpr long long kBtMinRatio = 3000;
-struct BtSlot {
-  int device = -1;
-  hipStream_t stream = nullptr;
-  void *data = nullptr;
-  size_t bytes = 0;
-};
-static BtSlot g_bt[kMaxPairSlots];
-// Held from choosing the buffer until the transpose and the product are
-// enqueued, so another thread cannot grow (free) the buffer of the same
-// stream in between; taken before g_pairs_mu, never while holding it.
-static std::mutex g_bt_mu;
-
-static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
-                           const BlockMatrix &c, hipStream_t stream) {
-  if (!tb || stream == hipStreamPerThread) return false;  // (many streams, one handle)
-  const long long min_mib = Knob(kKnobSddBtMinMib);
-  if (min_mib <= 0) return false;
-  const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
-  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
-  const long long blocks = c.nonzeros / (kBlock * kBlock);
-  if (blocks * 16384 < kBtMinRatio * n) return false;
-  unsigned long long id = 0;
-  if (CaptureState(stream, &id) != 0) return false;
-  GemmParams p;
-  const Matrix bt((int)k, (int)n, b.data);
-  return PrepareSdd(a, ta, bt, false, c, &p) == Status::kOk && UseGroupedSdd(&p, c, false) &&
-         Dsd4wEnabled() && Sdd4wApplies(p, true, ta, false, blocks);
-}
-
-// The transposed-B buffer of (device, stream), at least `bytes` (nullptr:
-// none -- the table is full or the allocation failed; the caller keeps the
-// NT / TT kernel). Caller holds g_bt_mu.
-static void *BtBuffer(hipStream_t stream, size_t bytes) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  BtSlot *slot = nullptr;
-  for (BtSlot &s : g_bt)
-    if (s.data != nullptr && s.device == dev && s.stream == stream) slot = &s;
-  if (slot == nullptr)
-    for (BtSlot &s : g_bt)
-      if (s.data == nullptr) {
-        slot = &s;
-        break;
-      }
-  if (slot == nullptr) return nullptr;
-  if (slot->bytes < bytes) {
-    if (slot->data != nullptr) {
-      // the stream's earlier launches may still read the old buffer
-      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
-      FreeQuiet(slot->data);
-      slot->data = nullptr;
-      slot->bytes = 0;
-    }
-    if (hipMalloc(&slot->data, bytes) != hipSuccess) {
-      slot->data = nullptr;
-      return nullptr;
-    }
-    slot->bytes = bytes;
-    slot->device = dev;
-    slot->stream = stream;
-  }
-  return slot->data;
 }
 
 hipError_t RunSdd(const Matrix &a, bool ta, const Matrix &b, bool tb,
@@ -1626,13 +1655,22 @@ int DdsPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
 // (dsd4w.hip), 2 the tall configuration, 3 split mode, 4 the tall
 // pipeline (4-wave, persistent), -1 rejected. Read-only:
 // it makes the workspace decisions a launch would make without allocating,
-// re-tying or advancing any workspace (safe during a capture).
+// re-tying or advancing any workspace (safe during a capture). (DSD NT
+// that transposes B first, UseBtTransposeDsd: the plan of the NN product
+// that follows.)
 int DsdPlan(const void *a, bool ta, const void *b, bool tb, const void *c,
             hipStream_t stream) {
   if (!a || !b || !c) return -1;
   GemmParams p;
   bool needs_meta = false;
   const BlockMatrix &am = *static_cast<const BlockMatrix *>(a);
+  const Matrix &bm = *static_cast<const Matrix *>(b);
+  if (UseBtTransposeDsd(am, ta, bm, tb, stream)) {
+    const Matrix bt(bm.cols, bm.rows, bm.data);
+    if (PrepareDsd(am, ta, bm, tb, *static_cast<const Matrix *>(c), &p, &needs_meta) ==
+        Status::kOk)
+      return DsdPlan(a, ta, &bt, false, c, stream);
+  }
   if (PrepareDsd(am, ta, *static_cast<const Matrix *>(b), tb,
                  *static_cast<const Matrix *>(c), &p, &needs_meta) != Status::kOk)
     return -1;

@@ -498,6 +498,24 @@ def test_kat_sdd_tail_split(ta, tb, case):
         sp.tuning("sdd_tail_min_k", prev)
 
 
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+@pytest.mark.parametrize("ex", [False, True])
+def test_kat_dsd_nt_bt_transpose(dtype, ex, bt_small):
+    """DSD NT over a dense A of >= 15000 rows (dispatch.cpp
+    UseBtTransposeDsd): B^T transposed into the library's buffer, then the
+    NN product; exact, Matmul and MatmulEx, and with the path off."""
+    got, want, (A, Bd, C) = kat_dsd(16384, 256, 2048, 1.0, False, True, dtype, ex=ex,
+                                    seed=51 + ex)
+    _equal(got, want, f"dsd nt bt {dtype} ex={ex}")
+    prev = sp.tuning("sdd_bt_min_mib", 0)
+    try:
+        got.fill_(float("nan"))
+        (sp.MatmulEx if ex else sp.Matmul)(A.m, False, Bd.m, True, C)
+        _equal(got, want, f"dsd nt bt off {dtype}")
+    finally:
+        sp.tuning("sdd_bt_min_mib", prev)
+
+
 def test_sdd_bt_two_threads_one_stream(bt_small):
     """Two host threads issue SDD NT on one stream, one of them with a larger
     B (so the stream's transposed-B buffer grows while the other thread's
