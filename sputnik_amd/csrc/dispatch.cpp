@@ -1128,7 +1128,10 @@ static bool UseBtTranspose(const Matrix &a, bool ta, const Matrix &b, bool tb,
   const long long min_mib = Knob(kKnobSddBtMinMib);
   if (min_mib <= 0) return false;
   const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
-  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
+  // (layout.hip moves 16-byte vectors: a 16-byte aligned B)
+  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20) ||
+      (reinterpret_cast<uintptr_t>(b.data) & 15) != 0)
+    return false;
   const long long blocks = c.nonzeros / (kBlock * kBlock);
   if (blocks * 16384 < kBtMinRatio * n) return false;
   unsigned long long id = 0;
@@ -1151,7 +1154,10 @@ static bool UseBtTransposeDsd(const BlockMatrix &a, bool ta, const Matrix &b, bo
   const long long min_mib = Knob(kKnobSddBtMinMib);
   if (min_mib <= 0) return false;
   const long long n = b.rows, k = b.cols;  // B^T stored [N][K]
-  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20)) return false;
+  // (layout.hip moves 16-byte vectors: a 16-byte aligned B)
+  if (n % 64 != 0 || k % 64 != 0 || n * k * 2 < (min_mib << 20) ||
+      (reinterpret_cast<uintptr_t>(b.data) & 15) != 0)
+    return false;
   const long long blocks = a.nonzeros / (kBlock * kBlock);
   if (blocks * 16384 < kDsdBtMinRatio * k) return false;
   unsigned long long id = 0;

@@ -516,6 +516,35 @@ def test_kat_dsd_nt_bt_transpose(dtype, ex, bt_small):
         sp.tuning("sdd_bt_min_mib", prev)
 
 
+def test_graph_capture_sdd_tail_split():
+    """The tail split's two launches (grouped 4-wave, then one-block 8-wave)
+    captured into one graph: replays exact."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(61)
+    m = n = 8192
+    A = IDense(m, 256, rng, "f16")
+    Bd = IDense(256, n, rng, "f16")
+    Cs = ISparse(m, n, 0.5, rng, "f16")
+    groups = int(((np.diff(Cs.offsets) + 3) // 4).sum())
+    assert 0 < groups % cus <= cus // 4, groups
+    sp.AllocateRowIndicesBuffer(Cs.m)
+    sp.RowIndices(Cs.m, Cs.m.row_indices)
+    want = _expect(Cs.blocks_of(A.values.astype(np.float64) @ Bd.values), "f16")
+    prev = sp.tuning("sdd_tail_min_k", 256)
+    try:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            sp.Matmul(A.m, False, Bd.m, False, Cs.m)
+        for _ in range(2):
+            Cs.dev.fill_(float("nan"))
+            g.replay()
+            _equal(Cs.dev, want, "captured sdd tail split")
+    finally:
+        sp.tuning("sdd_tail_min_k", prev)
+
+
 def test_sdd_bt_two_threads_one_stream(bt_small):
     """Two host threads issue SDD NT on one stream, one of them with a larger
     B (so the stream's transposed-B buffer grows while the other thread's
