@@ -53,7 +53,7 @@ def main():
                     "-I" + os.path.join(ROOT, "include"), "-Wno-unused-function",
                     "-c", os.path.join(d, "dsd4w.hip"), "-o", obj], check=True)
     b = os.path.join(ROOT, "build", "sputnik_amd")
-    objs = [os.path.join(b, f + ".o") for f in ("block_gemm", "metadata", "dispatch", "c_api")]
+    objs = [os.path.join(b, f + ".o") for f in ("block_gemm", "metadata", "layout", "dispatch", "c_api")]
     subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o",
                     os.path.join(ROOT, "build", "exp", name + ".so"), obj] + objs, check=True)
     print(name, "loads modified:", n)
